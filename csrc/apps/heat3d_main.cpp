@@ -1,0 +1,99 @@
+// heat3d-mi355x — command line driver.
+//
+//   heat3d NX NY NZ ITER_MAX EPS [--flags]
+//
+// Same positional contract, banner and run report as the reference
+// (heat3D.cu:270-315 and 1078-1106; exact formats in SURVEY.md App. B.4).
+// Multi-process runs read RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR /
+// MASTER_PORT (torchrun or mpirun env); every rank validates the command line
+// (the reference only checked argc on rank 0).
+#include <cstdio>
+#include <cstdlib>
+#include <exception>
+#include <iostream>
+
+#include "../core/config.hpp"
+#include "../io/io.hpp"
+#include "../runtime/solver.hpp"
+
+using namespace heat3d;
+
+int main(int argc, char** argv) {
+  Config cfg;
+  try {
+    cfg = Config::parse(argc, argv);
+  } catch (const UsageError& e) {
+    const char* r = std::getenv("RANK");
+    if (!r || std::atoi(r) == 0) {
+      std::cout << Config::usage() << std::flush;
+      std::cerr << "heat3d: " << e.what() << std::endl;
+    }
+    return 1;
+  }
+  try {
+    auto solver = make_solver_from_env(cfg);
+    const bool root = solver->is_root();
+    if (root && !cfg.quiet) std::cout << cfg.echo_banner() << std::flush;
+    solver->initialize();
+    RunResult r = solver->run();
+    double gerr = 0, lerr = 0;
+    solver->compute_error(&gerr, &lerr);
+    if (root) {
+      std::printf("Computational time (parallel): %.6f\n\n", r.seconds);
+      if (r.converged)
+        std::printf("Simulation has converged in %lld iterations with a convergence threshold of %e\n",
+                    (long long)r.conv_iter, cfg.eps);
+      else
+        std::printf("Simulation did not converge within %lld iterations.\n", (long long)cfg.iter_max);
+      std::printf("L2-norm error: %.4f %%\n", 100.0 * (cfg.compat ? lerr : gerr));
+      if (!cfg.compat) {
+        const auto& d = solver->decomposition();
+        std::printf("heat3d: backend=%s comm=%s ranks=%d dims=%dx%dx%d dtype=%s kernel=%s "
+                    "iterations=%lld issued=%lld GLUPS=%.3f norm=%.6e last_residual=%.6e\n",
+                    solver->backend().name(), solver->comm().name(), solver->comm().size(),
+                    d.topo.dims[0], d.topo.dims[1], d.topo.dims[2], dtype_name(cfg.dtype),
+                    solver->kernel_name().c_str(), (long long)r.iterations, (long long)r.issued,
+                    r.glups, r.norm, r.last_residual);
+      }
+      if (r.fault) std::fprintf(stderr, "heat3d: non-finite residual detected at iteration %lld\n",
+                                (long long)r.conv_iter);
+      std::fflush(stdout);
+    }
+    // output/out.dat (heat3D.cu:1109-1179): on by default for small grids
+    std::string out = cfg.output;
+    const double pts = (double)cfg.n[0] * cfg.n[1] * cfg.n[2];
+    if (out == "auto") out = pts <= 2.2e6 ? "output/out.dat" : "none";
+    if (out != "none") solver->write_tecplot(out, cfg.tecplot_layout);
+    if (!cfg.json_out.empty() && root) {
+      io::Json j;
+      j.set_raw("N", "[" + std::to_string(cfg.n[0]) + ", " + std::to_string(cfg.n[1]) + ", " +
+                         std::to_string(cfg.n[2]) + "]");
+      j.set("dtype", std::string(dtype_name(cfg.dtype)));
+      j.set("backend", std::string(solver->backend().name()));
+      j.set("comm", std::string(solver->comm().name()));
+      j.set("ranks", (int64_t)solver->comm().size());
+      const auto& d = solver->decomposition();
+      j.set_raw("dims", "[" + std::to_string(d.topo.dims[0]) + ", " + std::to_string(d.topo.dims[1]) +
+                            ", " + std::to_string(d.topo.dims[2]) + "]");
+      j.set("kernel", solver->kernel_name());
+      j.set("eps", cfg.eps);
+      j.set("iter_max", (int64_t)cfg.iter_max);
+      j.set_bool("converged", r.converged);
+      j.set("conv_iter", (int64_t)r.conv_iter);
+      j.set("iterations", (int64_t)r.iterations);
+      j.set("issued", (int64_t)r.issued);
+      j.set("seconds", r.seconds);
+      j.set("glups", r.glups);
+      j.set("norm", r.norm);
+      j.set("last_residual", r.last_residual);
+      j.set("error_percent", 100.0 * gerr);
+      j.set("error_percent_rank0_local", 100.0 * lerr);
+      j.set_bool("fault", r.fault);
+      io::write_file_atomic(cfg.json_out, j.dump() + "\n");
+    }
+    return r.fault ? 3 : 0;
+  } catch (const std::exception& e) {
+    std::cerr << "heat3d: error: " << e.what() << std::endl;
+    return 2;
+  }
+}

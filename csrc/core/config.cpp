@@ -1,0 +1,215 @@
+#include "config.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <iomanip>
+#include <sstream>
+
+namespace heat3d {
+
+const char* face_name(Face f) {
+  static const char* names[] = {"LEFT", "RIGHT", "BOTTOM", "TOP", "BACK", "FRONT"};
+  return names[static_cast<int>(f)];
+}
+
+const char* dtype_name(DType t) { return t == DType::F64 ? "fp64" : "fp32"; }
+
+DType parse_dtype(const std::string& s) {
+  if (s == "fp64" || s == "f64" || s == "double" || s == "float64") return DType::F64;
+  if (s == "fp32" || s == "f32" || s == "float" || s == "float32") return DType::F32;
+  throw UsageError("unknown dtype '" + s + "' (use fp64 or fp32)");
+}
+
+std::string Box::str() const {
+  std::ostringstream os;
+  os << "[" << lo[0] << "," << hi[0] << ")x[" << lo[1] << "," << hi[1] << ")x[" << lo[2]
+     << "," << hi[2] << ")";
+  return os.str();
+}
+
+Physics Physics::make(int64_t nx, int64_t ny, int64_t nz) {
+  Physics p;
+  p.n[0] = nx;
+  p.n[1] = ny;
+  p.n[2] = nz;
+  for (int a = 0; a < 3; ++a) {
+    HEAT3D_CHECK(p.n[a] >= 3, "grid needs at least 3 vertices per axis, got " << p.n[a]);
+    // heat3D.cu:352-355: spacing = L / (N - 1.0)
+    p.h[a] = p.length[a] / static_cast<double>(static_cast<double>(p.n[a]) - 1.0);
+  }
+  const double hmin = std::min({p.h[0], p.h[1], p.h[2]});
+  // heat3D.cu:359-360: dt = CFL * 1.0 / (3 * 2) * pow(min(h), 2.0) / alpha
+  p.dt = p.cfl * 1.0 / (3 * 2) * std::pow(hmin, 2.0) / p.alpha;
+  // heat3D.cu:365-367: D = dt * alpha / pow(h, 2.0)
+  for (int a = 0; a < 3; ++a) p.D[a] = p.dt * p.alpha / std::pow(p.h[a], 2.0);
+  return p;
+}
+
+std::array<int, 3> parse_decomp(const std::string& s) {
+  std::array<int, 3> d = {0, 0, 0};
+  int idx = 0;
+  std::string cur;
+  for (char c : s + "x") {
+    if (c == 'x' || c == 'X' || c == ',') {
+      if (idx >= 3 || cur.empty()) throw UsageError("bad --decomp '" + s + "' (want AxBxC)");
+      d[idx++] = std::atoi(cur.c_str());
+      cur.clear();
+    } else if (c >= '0' && c <= '9') {
+      cur += c;
+    } else {
+      throw UsageError("bad --decomp '" + s + "' (want AxBxC)");
+    }
+  }
+  if (idx != 3 || d[0] < 1 || d[1] < 1 || d[2] < 1)
+    throw UsageError("bad --decomp '" + s + "' (want AxBxC, each >= 1)");
+  return d;
+}
+
+std::string Config::usage() {
+  // Text of heat3D.cu:286-290 followed by the framework's flags.
+  std::ostringstream os;
+  os << "Incorrect number of command line arguments specified, use the following syntax:\n\n"
+     << "bin/HeatEquation3D NUM_CELLS_X NUM_CELLS_Y NUM_CELLS_Z ITER_MAX EPS\n"
+     << "\nor, using MPI, use the following syntax:\n\n"
+     << "mpirun -n NUM_PROCS bin/HeatEquation3D NUM_CELLS_X NUM_CELLS_Y NUM_CELLS_Z ITER_MAX EPS\n"
+     << "\nSee source code for additional informations!\n"
+     << "\nheat3d (MI355X) options:\n"
+     << "  --dtype fp64|fp32         compute precision (default fp64)\n"
+     << "  --backend auto|hip|cpu    compute backend (default: hip when a GPU is visible)\n"
+     << "  --comm auto|none|local|rccl|socket\n"
+     << "                            halo/reduction transport (auto: rccl for multi-process\n"
+     << "                            GPU runs, socket for multi-process CPU runs)\n"
+     << "  --decomp AxBxC            process grid (default: balanced MPI_Dims_create split)\n"
+     << "  --virtual-ranks P         P subdomains in one process (LocalComm)\n"
+     << "  --device N                GPU ordinal (default LOCAL_RANK)\n"
+     << "  --graph / --no-graph      capture iterations in hipGraphs (default on)\n"
+     << "  --no-overlap              do not split interior/boundary work\n"
+     << "  --check-every K           host poll period of the device convergence flag\n"
+     << "  --kernel NAME             stencil kernel variant (auto|naive|column[:V:R:L])\n"
+     << "  --output PATH|none        Tecplot output (default output/out.dat for small grids)\n"
+     << "  --tecplot-layout auto|ref|owned\n"
+     << "  --compat                  reproduce reference reporting quirks\n"
+     << "  --checkpoint-every K --checkpoint-dir DIR   periodic binary checkpoints\n"
+     << "  --restart DIR             resume from a checkpoint directory\n"
+     << "  --json-out PATH           write a JSON run report\n"
+     << "  --verbose N               print residual every N iterations\n"
+     << "  --threads N               CPU backend OpenMP threads\n"
+     << "  --quiet                   suppress the banner\n";
+  return os.str();
+}
+
+static int64_t to_i64(const std::string& s, const char* what) {
+  try {
+    size_t pos = 0;
+    long long v = std::stoll(s, &pos);
+    if (pos != s.size()) throw std::invalid_argument(s);
+    return v;
+  } catch (const std::exception&) {
+    throw UsageError(std::string("invalid integer for ") + what + ": '" + s + "'");
+  }
+}
+
+static double to_f64(const std::string& s, const char* what) {
+  try {
+    size_t pos = 0;
+    double v = std::stod(s, &pos);
+    if (pos != s.size()) throw std::invalid_argument(s);
+    return v;
+  } catch (const std::exception&) {
+    throw UsageError(std::string("invalid number for ") + what + ": '" + s + "'");
+  }
+}
+
+Config Config::parse(int argc, const char* const* argv) {
+  Config c;
+  if (argc > 0 && argv[0]) c.argv0 = argv[0];
+  std::vector<std::string> pos;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto need = [&](const char* flag) -> std::string {
+      if (i + 1 >= argc) throw UsageError(std::string("missing value for ") + flag);
+      return argv[++i];
+    };
+    // accept --flag=value too
+    std::string val;
+    auto eq = a.find('=');
+    bool has_eq = a.rfind("--", 0) == 0 && eq != std::string::npos;
+    std::string key = has_eq ? a.substr(0, eq) : a;
+    auto get = [&](const char* flag) { return has_eq ? a.substr(eq + 1) : need(flag); };
+    if (key.rfind("--", 0) != 0) {
+      pos.push_back(a);
+      continue;
+    }
+    if (key == "--dtype") c.dtype = parse_dtype(get("--dtype"));
+    else if (key == "--backend") {
+      std::string v = get("--backend");
+      if (v == "auto") c.backend = BackendKind::Auto;
+      else if (v == "hip" || v == "gpu") c.backend = BackendKind::Hip;
+      else if (v == "cpu") c.backend = BackendKind::Cpu;
+      else throw UsageError("unknown backend '" + v + "'");
+    } else if (key == "--comm") {
+      std::string v = get("--comm");
+      if (v == "auto") c.comm = CommKind::Auto;
+      else if (v == "none") c.comm = CommKind::None;
+      else if (v == "local") c.comm = CommKind::Local;
+      else if (v == "rccl" || v == "nccl") c.comm = CommKind::Rccl;
+      else if (v == "socket" || v == "tcp") c.comm = CommKind::Socket;
+      else throw UsageError("unknown comm '" + v + "'");
+    } else if (key == "--decomp") c.decomp = parse_decomp(get("--decomp"));
+    else if (key == "--virtual-ranks") c.virtual_ranks = (int)to_i64(get("--virtual-ranks"), "--virtual-ranks");
+    else if (key == "--device") c.device = (int)to_i64(get("--device"), "--device");
+    else if (key == "--graph") c.use_graph = true;
+    else if (key == "--no-graph") c.use_graph = false;
+    else if (key == "--overlap") c.overlap = true;
+    else if (key == "--no-overlap") c.overlap = false;
+    else if (key == "--check-every") c.check_every = (int)to_i64(get("--check-every"), "--check-every");
+    else if (key == "--graph-chunk") c.graph_chunk = (int)to_i64(get("--graph-chunk"), "--graph-chunk");
+    else if (key == "--kernel") c.kernel = get("--kernel");
+    else if (key == "--output") c.output = get("--output");
+    else if (key == "--tecplot-layout") c.tecplot_layout = get("--tecplot-layout");
+    else if (key == "--compat") c.compat = true;
+    else if (key == "--checkpoint-every") c.checkpoint_every = to_i64(get("--checkpoint-every"), "--checkpoint-every");
+    else if (key == "--checkpoint-dir") c.checkpoint_dir = get("--checkpoint-dir");
+    else if (key == "--restart") c.restart = get("--restart");
+    else if (key == "--json-out") c.json_out = get("--json-out");
+    else if (key == "--verbose") c.verbose = (int)to_i64(get("--verbose"), "--verbose");
+    else if (key == "--threads") c.cpu_threads = (int)to_i64(get("--threads"), "--threads");
+    else if (key == "--quiet") c.quiet = true;
+    else if (key == "--help") throw UsageError("help requested");
+    else throw UsageError("unknown option '" + a + "'");
+  }
+  if (pos.size() != 5)
+    throw UsageError("expected 5 positional arguments (NX NY NZ ITER_MAX EPS), got " +
+                     std::to_string(pos.size()));
+  c.n[0] = to_i64(pos[0], "NUM_CELLS_X");
+  c.n[1] = to_i64(pos[1], "NUM_CELLS_Y");
+  c.n[2] = to_i64(pos[2], "NUM_CELLS_Z");
+  c.iter_max = to_i64(pos[3], "ITER_MAX");
+  c.eps = to_f64(pos[4], "EPS");
+  c.eps_text = pos[4];
+  for (int a = 0; a < 3; ++a)
+    if (c.n[a] < 3) throw UsageError("each grid extent must be >= 3");
+  if (c.iter_max < 0) throw UsageError("ITER_MAX must be >= 0");
+  if (c.virtual_ranks < 1) throw UsageError("--virtual-ranks must be >= 1");
+  if (c.check_every < 1) c.check_every = 1;
+  if (c.graph_chunk < 2) c.graph_chunk = 2;
+  if (c.graph_chunk % 2) c.graph_chunk += 1;
+  return c;
+}
+
+std::string Config::echo_banner() const {
+  // heat3D.cu:293-302 (including the "Runnung" typo and trailing space, B.4).
+  std::ostringstream os;
+  os << "Runnung HeatEquation3D with the following arguments: \n";
+  os << "executable:               " << argv0 << "\n";
+  os << "number of cells in x:     " << n[0] << "\n";
+  os << "number of cells in y:     " << n[1] << "\n";
+  os << "number of cells in z:     " << n[2] << "\n";
+  os << "max number of iterations: " << iter_max << "\n";
+  os << "convergence threshold:    " << eps << "\n\n";
+  return os.str();
+}
+
+}  // namespace heat3d

@@ -1,0 +1,77 @@
+// heat3d-mi355x — run configuration, physics constants, CLI parsing.
+//
+// The positional contract `NX NY NZ ITER_MAX EPS` is the reference's
+// (heat3D.cu:270-315); physics constants follow heat3D.cu:331-367
+// (unit cube, alpha = 1, CFL = 0.4, dt = CFL/6 * min(h)^2, D_d = dt/h_d^2).
+// Long flags are new (SURVEY.md §5 "Config / flag system").
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace heat3d {
+
+struct Physics {
+  int64_t n[3] = {0, 0, 0};      // global vertex counts
+  double length[3] = {1.0, 1.0, 1.0};
+  double alpha = 1.0;
+  double cfl = 0.4;
+  double h[3] = {0, 0, 0};       // spacing
+  double dt = 0;
+  double D[3] = {0, 0, 0};       // dt * alpha / h^2 per axis
+
+  static Physics make(int64_t nx, int64_t ny, int64_t nz);
+};
+
+enum class BackendKind { Auto, Hip, Cpu };
+enum class CommKind { Auto, None, Local, Rccl, Socket };
+
+struct Config {
+  // --- reference positional arguments
+  int64_t n[3] = {0, 0, 0};
+  int64_t iter_max = 0;
+  double eps = 0.0;
+  std::string eps_text;        // as typed, for the echo banner
+  std::string argv0 = "heat3d";
+
+  // --- framework flags
+  DType dtype = DType::F64;
+  BackendKind backend = BackendKind::Auto;
+  CommKind comm = CommKind::Auto;
+  std::array<int, 3> decomp = {0, 0, 0};  // 0 = choose with dims_create
+  int virtual_ranks = 1;                  // LocalComm: P subdomains in one process
+  int device = -1;                        // -1: LOCAL_RANK or 0
+  bool use_graph = true;
+  bool overlap = true;
+  int check_every = 64;                   // host poll period for the device convergence flag
+  int graph_chunk = 32;                   // iterations per captured hipGraph (rounded to even)
+  std::string kernel = "auto";            // stencil kernel variant
+  std::string output = "auto";            // path | none | auto (output/out.dat when small)
+  std::string tecplot_layout = "auto";    // auto | ref | owned
+  bool compat = false;                    // reproduce reference reporting quirks
+  int64_t checkpoint_every = 0;
+  std::string checkpoint_dir;
+  std::string restart;
+  std::string json_out;
+  int verbose = 0;
+  bool quiet = false;
+  int cpu_threads = 0;
+
+  // Parse argv.  Throws UsageError on a malformed command line.
+  static Config parse(int argc, const char* const* argv);
+  static std::string usage();
+  std::string echo_banner() const;  // the reference's "Runnung ..." block (B.4)
+};
+
+class UsageError : public Error {
+ public:
+  explicit UsageError(const std::string& m) : Error(m) {}
+};
+
+std::array<int, 3> parse_decomp(const std::string& s);
+
+}  // namespace heat3d

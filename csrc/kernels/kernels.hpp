@@ -1,0 +1,112 @@
+// heat3d-mi355x — kernel launch API, implemented twice:
+//   heat3d::hip::*  hand-written gfx950 kernels (kernels_hip.hip)
+//   heat3d::cpu::*  OpenMP host kernels used by the CPU backend / oracle (kernels_cpu.cpp)
+//
+// Both evaluate the FTCS update with the reference's per-cell expression order
+// (heat3D.cu:128-131) and with floating-point contraction
+// disabled, so the GPU and CPU backends agree bit for bit.
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+#include "../core/common.hpp"
+#include "layout.hpp"
+
+namespace heat3d {
+
+struct KernelSpec {
+  enum Kind { Naive = 0, Column = 1 } kind = Column;
+  int V = 0;  // elements per lane along z (0 = default for dtype)
+  int R = 0;  // rows per wave along y (0 = default)
+  int L = 0;  // x-segment length per wave (0 = auto)
+  static KernelSpec parse(const std::string& s);
+  std::string str() const;
+};
+
+struct StencilParams {
+  const void* in = nullptr;
+  void* out = nullptr;
+  Layout L;
+  Box box;                  // local owned coordinates to update
+  double D[3] = {0, 0, 0};  // Dx, Dy, Dz
+  DeviceState* state = nullptr;
+  int slot = 0;             // residual parity slot
+};
+
+struct InitParams {
+  void* field = nullptr;
+  Layout L;
+  int64_t gstart[3] = {0, 0, 0};  // global index of owned (0,0,0)
+  int64_t N[3] = {0, 0, 0};
+  double h[3] = {0, 0, 0};
+};
+
+// Apply the Dirichlet boundary value at a global vertex (heat3D.cu:414-453
+// order: TOP (y = 1) <- 1.0, then LEFT/RIGHT/BACK/FRONT <- y overwrite,
+// BOTTOM stays 0; interior 0).
+H3D_HD inline double boundary_value(int64_t gi, int64_t gj, int64_t gk, const int64_t N[3],
+                             const double h[3]) {
+  if (gi == 0 || gi == N[0] - 1 || gk == 0 || gk == N[2] - 1)
+    return static_cast<double>(gj) * h[1];
+  if (gj == N[1] - 1) return 1.0;
+  return 0.0;
+}
+
+namespace hip {
+void init_field(DType t, const InitParams& p, void* stream);
+void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, void* stream);
+void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, void* stream);
+void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
+              const Layout& Ld, const Box& bd, void* stream);
+void check_convergence(DeviceState* s, int slot, void* stream);
+// Adds Σ|T - y| and the point count over `box` into s->error_sum/error_count.
+// `scratch` must hold at least error_scratch_elems() doubles.
+void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
+                      const int64_t gstart[3], double hy, double* scratch, DeviceState* s,
+                      void* stream);
+int64_t error_scratch_elems();
+// Fault injection (tests): write `value` at local owned point (i,j,k).
+void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k, double value,
+          void* stream);
+}  // namespace hip
+
+namespace cpu {
+void set_threads(int n);
+void init_field(DType t, const InitParams& p);
+void stencil(DType t, const StencilParams& p);
+void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf);
+void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf);
+void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
+              const Layout& Ld, const Box& bd);
+void check_convergence(DeviceState* s, int slot);
+void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
+                      const int64_t gstart[3], double hy, DeviceState* s);
+void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k, double value);
+}  // namespace cpu
+
+// Shared scalar logic of the convergence check (heat3D.cu:1026-1073 with the
+// survey's fixes: global norm, global max residual).  Used verbatim by the
+// CPU backend and mirrored by the single-thread HIP kernel.
+H3D_HD inline void check_convergence_scalar(DeviceState* s, double r) {
+  const int64_t t = s->iter;
+  if (s->hist_cap > 0) s->hist[t % s->hist_cap] = r;
+  if (!s->done) {
+    s->last_residual = r;
+    if (!(r == r) || r > 1.7976931348623157e308) {  // NaN or Inf
+      s->fault = 1;
+      s->done = 1;
+      s->conv_iter = t;
+    } else {
+      if (t == 0 && r != 0.0) s->norm = r;
+      if (r / s->norm < s->eps) {
+        s->done = 1;
+        s->conv_iter = t;
+      }
+    }
+  }
+  s->iter = t + 1;
+}
+
+}  // namespace heat3d

@@ -1,0 +1,540 @@
+// heat3d-mi355x — hand-written gfx950 (CDNA4) kernels.
+//
+// Replaces the reference's single CUDA kernel `computeT` (heat3D.cu:118-142:
+// one thread per x plane, 2-thread blocks, triple pointer chasing, never
+// terminating k loop — SURVEY.md §2.2) and the host loop nests around it
+// (T0 = T copy, face pack, residual scan, error scan: heat3D.cu:541-1106).
+//
+// Hot kernel: `stencil_column<Real,V,R>` — 2.5D blocking for a 7-point FTCS
+// update that is HBM-bound (16 B/point fp64, 8 B/point fp32):
+//   * one wave64 owns a (R rows in y) x (64*V points in z) column tile and
+//     marches along x over a segment of planes;
+//   * the x-1 / x / x+1 planes live in a register queue, prefetched one plane
+//     ahead, so every interior value is read from HBM exactly once;
+//   * z neighbours come from neighbouring lanes through DPP wave_shr/wave_shl
+//     (no LDS, no barriers), the two tile-edge values from one cooperative
+//     load + v_readlane;
+//   * y neighbours inside the tile are registers; the two tile-halo rows are
+//     re-read from L2 (shared with the y-adjacent wave, which the XCD-aware
+//     block remap keeps on the same XCD);
+//   * 16-byte vector loads/stores (rows are 128-B aligned, see layout.hpp);
+//   * the convergence residual max|T^{n+1}-T^n| is fused: wave max-reduce,
+//     one 64-bit atomic max per wave;
+//   * a device flag set by the convergence check turns the kernel into a
+//     no-op, so over-issued / graph-replayed iterations are harmless.
+// Floating-point contraction is disabled so results are bitwise identical to
+// the CPU backend (kernels_cpu.cpp) and independent of the decomposition.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+
+#include "kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace heat3d {
+namespace hip {
+
+#define HIPK_CHECK(expr)                                                             \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) HEAT3D_THROW("HIP error " << hipGetErrorString(_e) << " at " #expr); \
+  } while (0)
+
+static inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+template <typename Real, int V>
+struct VecOf;
+template <> struct VecOf<double, 1> { typedef double type; };
+template <> struct VecOf<double, 2> { typedef double type __attribute__((ext_vector_type(2))); };
+template <> struct VecOf<float, 1> { typedef float type; };
+template <> struct VecOf<float, 2> { typedef float type __attribute__((ext_vector_type(2))); };
+template <> struct VecOf<float, 4> { typedef float type __attribute__((ext_vector_type(4))); };
+
+template <typename Real>
+__device__ __forceinline__ Real ftcs(Real c, Real xm, Real xp, Real ym, Real yp, Real zm, Real zp,
+                                     Real Dx, Real Dy, Real Dz) {
+#pragma clang fp contract(off)
+  const Real c2 = Real(2) * c;
+  const Real ax = (xp - c2) + xm;
+  const Real ay = (yp - c2) + ym;
+  const Real az = (zp - c2) + zm;
+  return ((c + Dx * ax) + Dy * ay) + Dz * az;
+}
+
+// ---- cross-lane helpers ----------------------------------------------------
+// DPP wave_shr:1 (0x138): lane i <- lane i-1 ; lane 0 keeps `old`.
+// DPP wave_shl:1 (0x130): lane i <- lane i+1 ; lane 63 keeps `old`.
+__device__ __forceinline__ double dpp_shr1(double old, double v) {
+  long long ov = __builtin_bit_cast(long long, old), vv = __builtin_bit_cast(long long, v);
+  int lo = __builtin_amdgcn_update_dpp((int)ov, (int)vv, 0x138, 0xf, 0xf, false);
+  int hi = __builtin_amdgcn_update_dpp((int)(ov >> 32), (int)(vv >> 32), 0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_shl1(double old, double v) {
+  long long ov = __builtin_bit_cast(long long, old), vv = __builtin_bit_cast(long long, v);
+  int lo = __builtin_amdgcn_update_dpp((int)ov, (int)vv, 0x130, 0xf, 0xf, false);
+  int hi = __builtin_amdgcn_update_dpp((int)(ov >> 32), (int)(vv >> 32), 0x130, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ float dpp_shr1(float old, float v) {
+  int r = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                      0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(float, r);
+}
+__device__ __forceinline__ float dpp_shl1(float old, float v) {
+  int r = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                      0x130, 0xf, 0xf, false);
+  return __builtin_bit_cast(float, r);
+}
+__device__ __forceinline__ double readlane(double v, int lane) {
+  long long b = __builtin_bit_cast(long long, v);
+  int lo = __builtin_amdgcn_readlane((int)b, lane);
+  int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ float readlane(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+
+// Residual max over non-negative doubles, done on their IEEE bit patterns:
+// integer order == double order, and a NaN (bits above +Inf) wins, so a
+// blown-up field reaches the convergence check as a fault.
+__device__ __forceinline__ double res_max(double m, double d) { return (d != d || d > m) ? d : m; }
+
+__device__ __forceinline__ void residual_commit(unsigned long long* slot, double m) {
+  unsigned long long b = (unsigned long long)__builtin_bit_cast(long long, m);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long q = __shfl_xor(b, o, 64);
+    b = q > b ? q : b;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(slot, b);
+}
+
+__device__ __forceinline__ bool flag_set(const int* done) {
+  return done != nullptr && __builtin_nontemporal_load(done) != 0;
+}
+
+// ---- naive kernel: one lane per (y,z) column, 7 global loads per point -----
+// Baseline and thin-box (boundary shell) kernel.  Block = 64 (z) x 4 (y).
+template <typename Real>
+__global__ __launch_bounds__(256) void stencil_naive(const Real* __restrict__ in,
+                                                     Real* __restrict__ out, Layout L, Box b,
+                                                     Real Dx, Real Dy, Real Dz,
+                                                     unsigned long long* res, const int* done) {
+  if (flag_set(done)) return;
+  const int64_t k = b.lo[2] + (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int64_t j = b.lo[1] + (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int64_t x0 = b.lo[0] + (int64_t)blockIdx.z * 64;
+  const int64_t x1 = min(x0 + 64, b.hi[0]);
+  double m = 0.0;
+  if (k < b.hi[2] && j < b.hi[1]) {
+    const int64_t sx = L.sx, sy = L.sy;
+    for (int64_t i = x0; i < x1; ++i) {
+      const int64_t c = L.index(i, j, k);
+      const Real T = in[c];
+      const Real nv = ftcs<Real>(T, in[c - sx], in[c + sx], in[c - sy], in[c + sy], in[c - 1],
+                                 in[c + 1], Dx, Dy, Dz);
+      out[c] = nv;
+      m = res_max(m, fabs((double)nv - (double)T));
+    }
+  }
+  if (res) residual_commit(res, m);
+}
+
+// ---- column kernel ----------------------------------------------------------
+struct ColumnGeom {
+  int64_t z0a;       // first z of tile 0 (box z0 rounded down to V)
+  int nzt, nyt, nxs; // tiles along z, y; segments along x
+  int seg;           // planes per x segment
+  int64_t nwaves;    // nzt * nyt * nxs
+  int xq, xr;        // XCD remap: nblocks = 8 * xq + xr
+};
+
+template <typename Real, int V, int R>
+__global__ __launch_bounds__(256) void stencil_column(const Real* __restrict__ in,
+                                                      Real* __restrict__ out, Layout L, Box b,
+                                                      ColumnGeom g, Real Dx, Real Dy, Real Dz,
+                                                      unsigned long long* res, const int* done) {
+  typedef typename VecOf<Real, V>::type Vec;
+  constexpr int TZ = 64 * V;
+  if (flag_set(done)) return;
+
+  // XCD-aware remap: blocks b and b+8 share an XCD under round-robin dispatch,
+  // so give each XCD a contiguous range of tiles (y-adjacent tiles share halo
+  // rows through that XCD's L2).  Performance only; any placement is correct.
+  const int blk = blockIdx.x;
+  const int xcd = blk & 7;
+  const int beff = xcd * g.xq + min(xcd, g.xr) + (blk >> 3);
+  int64_t t = (int64_t)beff * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (t >= g.nwaves) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const int yt = (int)(t % g.nyt);
+  t /= g.nyt;
+  const int zt = (int)(t % g.nzt);
+  const int xs = (int)(t / g.nzt);
+
+  const int64_t kb = g.z0a + (int64_t)zt * TZ;  // tile's first z
+  const int64_t k = kb + (int64_t)lane * V;     // this lane's first z
+  const int64_t yb = b.lo[1] + (int64_t)yt * R;
+  const int ract = (int)min((int64_t)R, b.hi[1] - yb);
+  const int64_t xa = b.lo[0] + (int64_t)xs * g.seg;
+  const int64_t xe = min(xa + (int64_t)g.seg, b.hi[0]);
+  const int64_t sx = L.sx, sy = L.sy;
+
+  // validity of this lane's V points
+  bool valid[V];
+  bool allvalid = true;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    valid[v] = (k + v >= b.lo[2]) && (k + v < b.hi[2]);
+    allvalid &= valid[v];
+  }
+
+  // lane's column base pointer for row yb, plane 0
+  const int64_t base0 = L.index(0, yb, k);
+  // edge loads: lanes [0,R) fetch left edges (z = kb-1) of row `lane`,
+  // lanes [32,32+R) right edges (z = kb+TZ) of row `lane-32`
+  const int er = lane < 32 ? lane : lane - 32;
+  const bool eload = er < ract;
+  const int64_t ebase = L.index(0, yb + er, lane < 32 ? kb - 1 : kb + TZ);
+
+  auto ld = [&](int64_t plane, int r) -> Vec {
+    return *reinterpret_cast<const Vec*>(in + base0 + plane * sx + (int64_t)r * sy);
+  };
+
+  Vec qm[R], qc[R], qp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (r < ract) {
+      qm[r] = ld(xa - 1, r);
+      qc[r] = ld(xa, r);
+      qp[r] = ld(xa + 1, r);
+    }
+  Vec hb = ld(xa, -1), ht = ld(xa, ract);
+  Real ed = eload ? in[ebase + xa * sx] : Real(0);
+
+  double m = 0.0;
+  for (int64_t x = xa; x < xe; ++x) {
+    // prefetch plane x+2 centres and plane x+1 halos/edges
+    Vec qn[R];
+    const bool more = x + 1 < xe;
+    Vec hbn, htn;
+    Real edn = Real(0);
+    if (more) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (r < ract) qn[r] = ld(x + 2, r);
+      hbn = ld(x + 1, -1);
+      htn = ld(x + 1, ract);
+      if (eload) edn = in[ebase + (x + 1) * sx];
+    }
+
+    Vec nvv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < ract) {
+        const Vec c = qc[r];
+        const Vec ym = r == 0 ? hb : qc[r > 0 ? r - 1 : 0];
+        const Vec yp = (r == ract - 1) ? ht : qc[r + 1 < R ? r + 1 : R - 1];
+        const Real left = readlane(ed, r);
+        const Real right = readlane(ed, 32 + r);
+        Vec zm, zp;
+        if constexpr (V == 1) {
+          zm = dpp_shr1(left, c);
+          zp = dpp_shl1(right, c);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            zm[v] = v == 0 ? dpp_shr1(left, c[V - 1]) : c[v - 1];
+            zp[v] = v == V - 1 ? dpp_shl1(right, c[0]) : c[v + 1];
+          }
+        }
+        Vec nv;
+        if constexpr (V == 1) {
+          nv = ftcs<Real>(c, qm[r], qp[r], ym, yp, zm, zp, Dx, Dy, Dz);
+          if (valid[0]) m = res_max(m, fabs((double)nv - (double)c));
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            nv[v] = ftcs<Real>(c[v], qm[r][v], qp[r][v], ym[v], yp[v], zm[v], zp[v], Dx, Dy, Dz);
+            if (valid[v]) m = res_max(m, fabs((double)nv[v] - (double)c[v]));
+          }
+        }
+        nvv[r] = nv;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < ract) {
+        Real* dst = out + base0 + x * sx + (int64_t)r * sy;
+        if (allvalid) {
+          *reinterpret_cast<Vec*>(dst) = nvv[r];
+        } else {
+          if constexpr (V == 1) {
+            if (valid[0]) dst[0] = nvv[r];
+          } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+              if (valid[v]) dst[v] = nvv[r][v];
+          }
+        }
+      }
+    }
+    // rotate the register queue
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      qm[r] = qc[r];
+      qc[r] = qp[r];
+      qp[r] = qn[r];
+    }
+    hb = hbn;
+    ht = htn;
+    ed = edn;
+  }
+  if (res) residual_commit(res, m);
+}
+
+// ---- launch helpers -----------------------------------------------------------
+template <typename Real>
+static void launch_naive(const StencilParams& p, hipStream_t s) {
+  const Box& b = p.box;
+  dim3 grid((unsigned)((b.extent(2) + 63) / 64), (unsigned)((b.extent(1) + 3) / 4),
+            (unsigned)((b.extent(0) + 63) / 64));
+  unsigned long long* res = p.state ? &p.state->residual[p.slot] : nullptr;
+  const int* done = p.state ? &p.state->done : nullptr;
+  hipLaunchKernelGGL(stencil_naive<Real>, grid, dim3(256), 0, s, static_cast<const Real*>(p.in),
+                     static_cast<Real*>(p.out), p.L, b, (Real)p.D[0], (Real)p.D[1], (Real)p.D[2],
+                     res, done);
+  HIPK_CHECK(hipGetLastError());
+}
+
+template <typename Real, int V, int R>
+static void launch_column(const StencilParams& p, int seg, hipStream_t s) {
+  const Box& b = p.box;
+  constexpr int TZ = 64 * V;
+  ColumnGeom g;
+  g.z0a = (b.lo[2] / V) * V;
+  g.nzt = (int)((b.hi[2] - g.z0a + TZ - 1) / TZ);
+  g.nyt = (int)((b.extent(1) + R - 1) / R);
+  if (seg <= 0) {
+    // aim for >= ~16k waves so that 256 CUs see several rounds
+    const int64_t cols = (int64_t)g.nzt * g.nyt;
+    int64_t want = std::max<int64_t>(1, 16384 / std::max<int64_t>(1, cols));
+    seg = (int)std::max<int64_t>(16, (b.extent(0) + want - 1) / want);
+  }
+  g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));
+  g.nxs = (int)((b.extent(0) + g.seg - 1) / g.seg);
+  g.nwaves = (int64_t)g.nzt * g.nyt * g.nxs;
+  const int W = 4;
+  const int64_t nblocks = (g.nwaves + W - 1) / W;
+  HEAT3D_CHECK(nblocks < (1LL << 31), "too many blocks");
+  g.xq = (int)(nblocks / 8);
+  g.xr = (int)(nblocks % 8);
+  unsigned long long* res = p.state ? &p.state->residual[p.slot] : nullptr;
+  const int* done = p.state ? &p.state->done : nullptr;
+  hipLaunchKernelGGL((stencil_column<Real, V, R>), dim3((unsigned)nblocks), dim3(64 * W), 0, s,
+                     static_cast<const Real*>(p.in), static_cast<Real*>(p.out), p.L, b, g,
+                     (Real)p.D[0], (Real)p.D[1], (Real)p.D[2], res, done);
+  HIPK_CHECK(hipGetLastError());
+}
+
+template <typename Real>
+static void dispatch_column(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
+  const int V = k.V ? k.V : (sizeof(Real) == 8 ? 2 : 4);
+  const int R = k.R ? k.R : 8;
+  // Thin boxes (boundary shell slabs) go to the naive kernel: a column tile
+  // would run mostly idle lanes / rows there.
+  if (p.box.extent(2) < 32 || p.box.extent(1) < 2) {
+    launch_naive<Real>(p, s);
+    return;
+  }
+#define H3D_COL(VV, RR)                                  \
+  if (V == VV && R == RR) {                              \
+    launch_column<Real, VV, RR>(p, k.L, s);              \
+    return;                                              \
+  }
+  H3D_COL(1, 4) H3D_COL(1, 8) H3D_COL(2, 4) H3D_COL(2, 6) H3D_COL(2, 8) H3D_COL(2, 12)
+  if constexpr (sizeof(Real) == 4) {
+    H3D_COL(4, 4) H3D_COL(4, 8)
+  }
+#undef H3D_COL
+  HEAT3D_THROW("unsupported column kernel variant V=" << V << " R=" << R << " for "
+               << (sizeof(Real) == 8 ? "fp64" : "fp32"));
+}
+
+void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
+  if (p.box.empty()) return;
+  if (k.kind == KernelSpec::Naive) {
+    if (t == DType::F64) launch_naive<double>(p, S(stream));
+    else launch_naive<float>(p, S(stream));
+  } else {
+    if (t == DType::F64) dispatch_column<double>(p, k, S(stream));
+    else dispatch_column<float>(p, k, S(stream));
+  }
+}
+
+// ---- init ---------------------------------------------------------------------
+template <typename Real>
+__global__ __launch_bounds__(256) void init_kernel(Real* f, Layout L, InitParams p) {
+  const int64_t ez = L.n[2] + 2;
+  const int64_t kk = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (kk >= ez) return;
+  const int64_t k = kk - 1, j = (int64_t)blockIdx.y - 1, i = (int64_t)blockIdx.z - 1;
+  const int64_t gi = p.gstart[0] + i, gj = p.gstart[1] + j, gk = p.gstart[2] + k;
+  const bool phys = gi == 0 || gi == p.N[0] - 1 || gj == 0 || gj == p.N[1] - 1 || gk == 0 ||
+                    gk == p.N[2] - 1;
+  f[L.index(i, j, k)] = phys ? (Real)boundary_value(gi, gj, gk, p.N, p.h) : Real(0);
+}
+
+void init_field(DType t, const InitParams& p, void* stream) {
+  HIPK_CHECK(hipMemsetAsync(p.field, 0, p.L.bytes(), S(stream)));
+  dim3 grid((unsigned)((p.L.n[2] + 2 + 255) / 256), (unsigned)(p.L.n[1] + 2),
+            (unsigned)(p.L.n[0] + 2));
+  if (t == DType::F64)
+    hipLaunchKernelGGL(init_kernel<double>, grid, dim3(256), 0, S(stream),
+                       static_cast<double*>(p.field), p.L, p);
+  else
+    hipLaunchKernelGGL(init_kernel<float>, grid, dim3(256), 0, S(stream),
+                       static_cast<float*>(p.field), p.L, p);
+  HIPK_CHECK(hipGetLastError());
+}
+
+// ---- box <-> buffer copies (halo pack/unpack, local exchange) ------------------
+// grid: x = z chunks of 256, y = rows (ey), z = planes (ex)
+template <typename Real, int DIR>
+__global__ __launch_bounds__(256) void box_copy_kernel(const Real* __restrict__ src,
+                                                       Real* __restrict__ dst, Layout Ls, Box bs,
+                                                       Layout Ld, Box bd) {
+  const int64_t ez = bs.extent(2);
+  const int64_t kz = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (kz >= ez) return;
+  const int64_t j = blockIdx.y, i = blockIdx.z;
+  const int64_t ey = bs.extent(1);
+  int64_t si, di;
+  if (DIR == 0) {  // field -> contiguous buffer
+    si = Ls.index(bs.lo[0] + i, bs.lo[1] + j, bs.lo[2] + kz);
+    di = (i * ey + j) * ez + kz;
+  } else if (DIR == 1) {  // buffer -> field
+    si = (i * ey + j) * ez + kz;
+    di = Ld.index(bd.lo[0] + i, bd.lo[1] + j, bd.lo[2] + kz);
+  } else {  // field -> field
+    si = Ls.index(bs.lo[0] + i, bs.lo[1] + j, bs.lo[2] + kz);
+    di = Ld.index(bd.lo[0] + i, bd.lo[1] + j, bd.lo[2] + kz);
+  }
+  dst[di] = src[si];
+}
+
+template <int DIR>
+static void box_copy(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
+                     const Layout& Ld, const Box& bd, hipStream_t s) {
+  if (bs.empty()) return;
+  HEAT3D_CHECK(bs.extent(1) < 65536 && bs.extent(0) < 65536, "box too large for copy grid");
+  dim3 grid((unsigned)((bs.extent(2) + 255) / 256), (unsigned)bs.extent(1), (unsigned)bs.extent(0));
+  if (t == DType::F64)
+    hipLaunchKernelGGL((box_copy_kernel<double, DIR>), grid, dim3(256), 0, s,
+                       static_cast<const double*>(src), static_cast<double*>(dst), Ls, bs, Ld, bd);
+  else
+    hipLaunchKernelGGL((box_copy_kernel<float, DIR>), grid, dim3(256), 0, s,
+                       static_cast<const float*>(src), static_cast<float*>(dst), Ls, bs, Ld, bd);
+  HIPK_CHECK(hipGetLastError());
+}
+
+void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, void* stream) {
+  box_copy<0>(t, f, L, b, buf, L, b, S(stream));
+}
+void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, void* stream) {
+  box_copy<1>(t, buf, L, b, f, L, b, S(stream));
+}
+void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
+              const Layout& Ld, const Box& bd, void* stream) {
+  HEAT3D_CHECK(bs.extent(0) == bd.extent(0) && bs.extent(1) == bd.extent(1) &&
+                   bs.extent(2) == bd.extent(2),
+               "copy_box extent mismatch " << bs.str() << " vs " << bd.str());
+  box_copy<2>(t, src, Ls, bs, dst, Ld, bd, S(stream));
+}
+
+// ---- convergence check (single lane) ------------------------------------------
+__global__ void check_kernel(DeviceState* s, int slot) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double r = __builtin_bit_cast(double, (long long)s->residual[slot]);
+  check_convergence_scalar(s, r);
+  s->residual[slot] = kResidualInitBits;
+}
+
+void check_convergence(DeviceState* s, int slot, void* stream) {
+  hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, S(stream), s, slot);
+  HIPK_CHECK(hipGetLastError());
+}
+
+// ---- error vs analytic steady state T = y -------------------------------------
+constexpr int kErrBlocks = 1024;
+int64_t error_scratch_elems() { return kErrBlocks; }
+
+template <typename Real>
+__global__ __launch_bounds__(256) void error_partial_kernel(const Real* f, Layout L, Box b,
+                                                            int64_t gj0, double hy,
+                                                            double* partial) {
+  __shared__ double red[4];
+  const int64_t ey = b.extent(1), ez = b.extent(2);
+  const int64_t rows = b.extent(0) * ey;
+  double s = 0.0;
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int64_t i = b.lo[0] + row / ey, j = b.lo[1] + row % ey;
+    const double y = (double)(gj0 + j) * hy;
+    const Real* p = f + L.index(i, j, b.lo[2]);
+    for (int64_t k = threadIdx.x; k < ez; k += 256) s += fabs((double)p[k] - y);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ void error_final_kernel(const double* partial, int n, double count, DeviceState* s) {
+  if (threadIdx.x != 0) return;
+  double acc = 0.0;
+  for (int i = 0; i < n; ++i) acc += partial[i];  // fixed order: deterministic
+  s->error_sum += acc;
+  s->error_count += count;
+}
+
+void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
+                      const int64_t gstart[3], double hy, double* scratch, DeviceState* s,
+                      void* stream) {
+  if (box.empty()) return;
+  if (t == DType::F64)
+    hipLaunchKernelGGL(error_partial_kernel<double>, dim3(kErrBlocks), dim3(256), 0, S(stream),
+                       static_cast<const double*>(f), L, box, gstart[1], hy, scratch);
+  else
+    hipLaunchKernelGGL(error_partial_kernel<float>, dim3(kErrBlocks), dim3(256), 0, S(stream),
+                       static_cast<const float*>(f), L, box, gstart[1], hy, scratch);
+  HIPK_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(error_final_kernel, dim3(1), dim3(64), 0, S(stream), scratch, kErrBlocks,
+                     (double)box.volume(), s);
+  HIPK_CHECK(hipGetLastError());
+}
+
+template <typename Real>
+__global__ void poke_kernel(Real* f, int64_t idx, double v) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) f[idx] = (Real)v;
+}
+
+void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k, double value,
+          void* stream) {
+  const int64_t idx = L.index(i, j, k);
+  if (t == DType::F64)
+    hipLaunchKernelGGL(poke_kernel<double>, dim3(1), dim3(64), 0, S(stream),
+                       static_cast<double*>(f), idx, value);
+  else
+    hipLaunchKernelGGL(poke_kernel<float>, dim3(1), dim3(64), 0, S(stream),
+                       static_cast<float*>(f), idx, value);
+  HIPK_CHECK(hipGetLastError());
+}
+
+}  // namespace hip
+}  // namespace heat3d

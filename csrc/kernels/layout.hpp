@@ -1,0 +1,75 @@
+// heat3d-mi355x — local array geometry and device-resident solver state.
+//
+// One subdomain's field is a single contiguous allocation (no double*** pointer
+// tables: reference heat3D.cu:60-111 / SURVEY.md C5, C15) holding the owned
+// block plus a one-cell ghost shell, z fastest (the reference's T[i][j][k]
+// order, heat3D.cu:394-406).  Rows are padded so that the first owned z point
+// of every row is 128-byte aligned; that lets the stencil kernels issue
+// 16-byte vector loads/stores on gfx950 without realignment.  All indices are
+// 64-bit (4096^3 > 2^32 points).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../core/common.hpp"
+
+namespace heat3d {
+
+struct Layout {
+  int64_t n[3] = {0, 0, 0};  // owned extents
+  int64_t sx = 0, sy = 0;    // element strides of x planes and y rows (z stride 1)
+  int64_t zoff = 0;          // offset of owned k = 0 inside a row
+  int64_t origin = 0;        // element index of owned (0,0,0)
+  int64_t elems = 0;         // allocation length in elements (includes tail pad)
+  int64_t esize = 8;
+
+  // i, j, k in [-1, n] (ghost shell included)
+  H3D_HD inline int64_t index(int64_t i, int64_t j, int64_t k) const {
+    return origin + i * sx + j * sy + k;
+  }
+  // Alignment in elements used for the row offset / pitch.
+  static int64_t align_elems(int64_t esize) { return 128 / esize; }
+  static Layout make(const int64_t n[3], int64_t esize) {
+    Layout L;
+    for (int a = 0; a < 3; ++a) L.n[a] = n[a];
+    L.esize = esize;
+    const int64_t A = align_elems(esize);
+    L.zoff = A;                                  // ghost k = -1 lives at A - 1
+    const int64_t need = A + n[2] + 1;           // through ghost k = nz
+    L.sy = ((need + A - 1) / A) * A;
+    // break power-of-two row pitches (HBM channel / cache-set aliasing)
+    if ((L.sy & (L.sy - 1)) == 0) L.sy += A;
+    L.sx = (n[1] + 2) * L.sy;
+    L.origin = L.sx + L.sy + L.zoff;
+    // tail pad: kernels may over-read up to one 256-wide z tile past a row end
+    L.elems = (n[0] + 2) * L.sx + 2 * L.sy + 1024;
+    return L;
+  }
+  std::size_t bytes() const { return static_cast<std::size_t>(elems * esize); }
+};
+
+// Device-resident convergence state.  One per process, shared by every local
+// subdomain.  The residual accumulators hold the IEEE bit pattern of a
+// non-negative double so that an unsigned 64-bit atomic max (and an RCCL
+// uint64 max all-reduce) is an exact max of the doubles.
+struct DeviceState {
+  unsigned long long residual[2];  // per-iteration-parity max |T^{n+1}-T^n|
+  double norm;                     // residual of iteration 0 (heat3D.cu:1026-1032)
+  double eps;
+  double last_residual;
+  double error_sum;                // Σ|T - y| over owned points (error report)
+  double error_count;
+  int64_t iter;                    // iterations checked so far (next index)
+  int64_t conv_iter;               // 0-based converged iteration, -1 until then
+  int32_t done;                    // convergence reached (or fault): stencils early-exit
+  int32_t fault;                   // 1 = NaN/Inf residual detected
+  int64_t hist_cap;                // residual history ring capacity
+  double hist[1024];               // residual history ring (index = iter % cap)
+};
+
+// Residual accumulator initial value: the reference starts the max at
+// numeric_limits<double>::min() (heat3D.cu:1019).
+constexpr unsigned long long kResidualInitBits = 0x0010000000000000ULL;  // DBL_MIN
+
+}  // namespace heat3d

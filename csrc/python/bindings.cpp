@@ -1,0 +1,366 @@
+// heat3d-mi355x — Python bindings (pybind11, no torch headers).
+//
+// Exposes the native runtime (Solver, topology, decomposition, RCCL/socket
+// bootstrap helpers) and the individual gfx950 / CPU kernels on raw pointers
+// so that the Python package can drive them on torch tensors
+// (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "../comm/comm.hpp"
+#include "../comm/net.hpp"
+#include "../core/config.hpp"
+#include "../core/decomp.hpp"
+#include "../runtime/solver.hpp"
+
+namespace py = pybind11;
+using namespace heat3d;
+
+namespace {
+
+Config parse_args(const std::vector<std::string>& args) {
+  std::vector<const char*> av;
+  av.push_back("heat3d");
+  for (auto& a : args) av.push_back(a.c_str());
+  return Config::parse((int)av.size(), av.data());
+}
+
+Box to_box(const std::array<int64_t, 6>& b) {
+  Box r;
+  for (int a = 0; a < 3; ++a) {
+    r.lo[a] = b[2 * a];
+    r.hi[a] = b[2 * a + 1];
+  }
+  return r;
+}
+
+Layout to_layout(const std::array<int64_t, 3>& n, int64_t esize) {
+  int64_t nn[3] = {n[0], n[1], n[2]};
+  return Layout::make(nn, esize);
+}
+
+py::dict layout_dict(const Layout& L) {
+  py::dict d;
+  d["n"] = py::make_tuple(L.n[0], L.n[1], L.n[2]);
+  d["sx"] = L.sx;
+  d["sy"] = L.sy;
+  d["zoff"] = L.zoff;
+  d["origin"] = L.origin;
+  d["elems"] = L.elems;
+  d["esize"] = L.esize;
+  return d;
+}
+
+py::dict sub_dict(const Subdomain& s) {
+  py::dict d;
+  d["rank"] = s.rank;
+  d["coords"] = py::make_tuple(s.coords[0], s.coords[1], s.coords[2]);
+  d["n"] = py::make_tuple(s.n[0], s.n[1], s.n[2]);
+  d["gstart"] = py::make_tuple(s.gstart[0], s.gstart[1], s.gstart[2]);
+  py::list nb;
+  for (int f = 0; f < kNumFaces; ++f) nb.append(s.neighbors[f]);
+  d["neighbors"] = nb;
+  Box e = s.extended_global();
+  d["extended"] = py::make_tuple(e.lo[0], e.hi[0], e.lo[1], e.hi[1], e.lo[2], e.hi[2]);
+  return d;
+}
+
+py::array_t<double> to_numpy(std::vector<double>&& v, std::vector<py::ssize_t> shape) {
+  auto* heap = new std::vector<double>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete static_cast<std::vector<double>*>(p); });
+  std::vector<py::ssize_t> strides(shape.size());
+  py::ssize_t st = sizeof(double);
+  for (int i = (int)shape.size() - 1; i >= 0; --i) {
+    strides[i] = st;
+    st *= shape[i];
+  }
+  return py::array_t<double>(shape, strides, heap->data(), owner);
+}
+
+std::unique_ptr<Solver> create_solver(const std::vector<std::string>& args, int rank, int size,
+                                      const std::string& comm_kind, py::bytes unique_id,
+                                      int listen_fd, const std::vector<std::string>& addrs,
+                                      int device) {
+  Config cfg = parse_args(args);
+  BackendKind bk = cfg.backend;
+  if (bk == BackendKind::Auto) bk = hip_device_count() > 0 ? BackendKind::Hip : BackendKind::Cpu;
+  int dev = device >= 0 ? device : (cfg.device >= 0 ? cfg.device : 0);
+  std::unique_ptr<Backend> be = bk == BackendKind::Hip ? make_hip_backend(dev) : make_cpu_backend(cfg.cpu_threads);
+  std::unique_ptr<Comm> comm;
+  int nranks = 1;
+  if (comm_kind == "local" || comm_kind == "none") {
+    nranks = cfg.virtual_ranks;
+    comm = make_local_comm(nranks);
+  } else if (comm_kind == "rccl") {
+    HEAT3D_CHECK(bk == BackendKind::Hip, "rccl comm needs the HIP backend");
+    comm = make_rccl_comm(rank, size, std::string(unique_id), dev);
+    nranks = size;
+  } else if (comm_kind == "socket") {
+    comm = make_socket_comm_from_table(rank, size, listen_fd, addrs);
+    nranks = size;
+  } else {
+    throw UsageError("unknown comm kind '" + comm_kind + "'");
+  }
+  std::array<int, 3> fixed = {0, 0, 0};
+  if (cfg.decomp[0] > 0) fixed = cfg.decomp;
+  auto dims = dims_create(nranks, fixed);
+  return std::unique_ptr<Solver>(new Solver(cfg, std::move(be), std::move(comm), dims));
+}
+
+DType dt_of(const std::string& s) { return parse_dtype(s); }
+
+StencilParams sparams(int64_t in_ptr, int64_t out_ptr, const std::array<int64_t, 3>& n,
+                      int64_t esize, const std::array<int64_t, 6>& box,
+                      const std::array<double, 3>& D, int64_t state_ptr, int slot) {
+  StencilParams p;
+  p.in = reinterpret_cast<const void*>(in_ptr);
+  p.out = reinterpret_cast<void*>(out_ptr);
+  p.L = to_layout(n, esize);
+  p.box = to_box(box);
+  for (int a = 0; a < 3; ++a) p.D[a] = D[a];
+  p.state = reinterpret_cast<DeviceState*>(state_ptr);
+  p.slot = slot;
+  return p;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_heat3d, m) {
+  m.doc() = "heat3d-mi355x native runtime (HIP/gfx950 kernels, RCCL/socket comm, solver)";
+  py::register_exception<UsageError>(m, "UsageError");
+  py::register_exception<Error>(m, "NativeError");
+
+  m.def("device_count", &hip_device_count);
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("rccl_version", &rccl_version);
+  m.def("socket_listen", []() {
+    int port = 0;
+    int fd = net::listen_on("0.0.0.0", 0, &port);
+    return py::make_tuple(fd, port);
+  });
+  m.def("usage", &Config::usage);
+  m.def("config_parse", [](const std::vector<std::string>& args) {
+    Config c = parse_args(args);
+    py::dict d;
+    d["n"] = py::make_tuple(c.n[0], c.n[1], c.n[2]);
+    d["iter_max"] = c.iter_max;
+    d["eps"] = c.eps;
+    d["dtype"] = dtype_name(c.dtype);
+    d["decomp"] = py::make_tuple(c.decomp[0], c.decomp[1], c.decomp[2]);
+    d["virtual_ranks"] = c.virtual_ranks;
+    d["use_graph"] = c.use_graph;
+    d["overlap"] = c.overlap;
+    d["check_every"] = c.check_every;
+    d["kernel"] = c.kernel;
+    d["output"] = c.output;
+    d["compat"] = c.compat;
+    d["banner"] = c.echo_banner();
+    return d;
+  });
+  m.def("physics", [](int64_t nx, int64_t ny, int64_t nz) {
+    Physics p = Physics::make(nx, ny, nz);
+    py::dict d;
+    d["h"] = py::make_tuple(p.h[0], p.h[1], p.h[2]);
+    d["dt"] = p.dt;
+    d["D"] = py::make_tuple(p.D[0], p.D[1], p.D[2]);
+    return d;
+  });
+  m.def("dims_create", [](int n, std::array<int, 3> fixed) { return dims_create(n, fixed); },
+        py::arg("nprocs"), py::arg("fixed") = std::array<int, 3>{0, 0, 0});
+  m.def("decomposition", [](std::array<int64_t, 3> N, std::array<int, 3> dims) {
+    int64_t n[3] = {N[0], N[1], N[2]};
+    Decomposition d = Decomposition::make(n, dims);
+    py::list out;
+    for (auto& s : d.subs) out.append(sub_dict(s));
+    return out;
+  });
+  m.def("split_interior", [](std::array<int64_t, 3> n, std::vector<int> neighbors) {
+    Subdomain s;
+    for (int a = 0; a < 3; ++a) s.n[a] = n[a];
+    for (int f = 0; f < kNumFaces; ++f) s.neighbors[f] = neighbors.at(f);
+    Box in;
+    std::vector<Box> shell;
+    Decomposition::split_interior(s, &in, &shell);
+    auto tup = [](const Box& b) { return py::make_tuple(b.lo[0], b.hi[0], b.lo[1], b.hi[1], b.lo[2], b.hi[2]); };
+    py::list sl;
+    for (auto& b : shell) sl.append(tup(b));
+    return py::make_tuple(tup(in), sl);
+  });
+  m.def("layout", [](std::array<int64_t, 3> n, int64_t esize) { return layout_dict(to_layout(n, esize)); });
+  m.def("boundary_value", [](int64_t i, int64_t j, int64_t k, std::array<int64_t, 3> N, std::array<double, 3> h) {
+    int64_t n[3] = {N[0], N[1], N[2]};
+    double hh[3] = {h[0], h[1], h[2]};
+    return boundary_value(i, j, k, n, hh);
+  });
+  m.attr("DEVICE_STATE_BYTES") = (int64_t)sizeof(DeviceState);
+  m.attr("RESIDUAL_INIT_BITS") = (unsigned long long)kResidualInitBits;
+
+  // --- raw kernels (pointers as ints; stream = hipStream_t as int) ----------
+  py::module_ hk = m.def_submodule("hip", "gfx950 kernels on device pointers");
+  hk.def("stencil", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
+                       std::array<int64_t, 6> box, std::array<double, 3> D, int64_t state_ptr, int slot,
+                       const std::string& kernel, int64_t stream) {
+    DType t = dt_of(dt);
+    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
+    hip::stencil(t, p, KernelSpec::parse(kernel), reinterpret_cast<void*>(stream));
+  });
+  hk.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
+                          std::array<int64_t, 3> N, std::array<double, 3> h, int64_t stream) {
+    DType t = dt_of(dt);
+    InitParams p;
+    p.field = reinterpret_cast<void*>(ptr);
+    p.L = to_layout(n, (int64_t)dtype_size(t));
+    for (int a = 0; a < 3; ++a) {
+      p.gstart[a] = gstart[a];
+      p.N[a] = N[a];
+      p.h[a] = h[a];
+    }
+    hip::init_field(t, p, reinterpret_cast<void*>(stream));
+  });
+  hk.def("pack_box", [](const std::string& dt, int64_t f, std::array<int64_t, 3> n, std::array<int64_t, 6> box,
+                        int64_t buf, int64_t stream) {
+    DType t = dt_of(dt);
+    hip::pack_box(t, reinterpret_cast<void*>(f), to_layout(n, (int64_t)dtype_size(t)), to_box(box),
+                  reinterpret_cast<void*>(buf), reinterpret_cast<void*>(stream));
+  });
+  hk.def("unpack_box", [](const std::string& dt, int64_t f, std::array<int64_t, 3> n, std::array<int64_t, 6> box,
+                          int64_t buf, int64_t stream) {
+    DType t = dt_of(dt);
+    hip::unpack_box(t, reinterpret_cast<void*>(f), to_layout(n, (int64_t)dtype_size(t)), to_box(box),
+                    reinterpret_cast<void*>(buf), reinterpret_cast<void*>(stream));
+  });
+  hk.def("check_convergence", [](int64_t state_ptr, int slot, int64_t stream) {
+    hip::check_convergence(reinterpret_cast<DeviceState*>(state_ptr), slot, reinterpret_cast<void*>(stream));
+  });
+
+  py::module_ ck = m.def_submodule("cpu", "OpenMP host kernels on host pointers");
+  ck.def("stencil", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
+                       std::array<int64_t, 6> box, std::array<double, 3> D, int64_t state_ptr, int slot) {
+    DType t = dt_of(dt);
+    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
+    py::gil_scoped_release nogil;
+    cpu::stencil(t, p);
+  });
+  ck.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
+                          std::array<int64_t, 3> N, std::array<double, 3> h) {
+    DType t = dt_of(dt);
+    InitParams p;
+    p.field = reinterpret_cast<void*>(ptr);
+    p.L = to_layout(n, (int64_t)dtype_size(t));
+    for (int a = 0; a < 3; ++a) {
+      p.gstart[a] = gstart[a];
+      p.N[a] = N[a];
+      p.h[a] = h[a];
+    }
+    cpu::init_field(t, p);
+  });
+
+  // --- solver ---------------------------------------------------------------
+  py::class_<Solver>(m, "Solver")
+      .def(py::init(&create_solver), py::arg("args"), py::arg("rank") = 0, py::arg("size") = 1,
+           py::arg("comm") = "local", py::arg("unique_id") = py::bytes(), py::arg("listen_fd") = -1,
+           py::arg("addrs") = std::vector<std::string>{}, py::arg("device") = -1)
+      .def("initialize", [](Solver& s) {
+        py::gil_scoped_release nogil;
+        s.initialize();
+      })
+      .def("run", [](Solver& s) {
+        RunResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = s.run();
+        }
+        py::dict d;
+        d["converged"] = r.converged;
+        d["fault"] = r.fault;
+        d["conv_iter"] = r.conv_iter;
+        d["iterations"] = r.iterations;
+        d["issued"] = r.issued;
+        d["seconds"] = r.seconds;
+        d["norm"] = r.norm;
+        d["last_residual"] = r.last_residual;
+        d["glups"] = r.glups;
+        return d;
+      })
+      .def("step", [](Solver& s, int64_t n) {
+        py::gil_scoped_release nogil;
+        s.step(n);
+      })
+      .def("synchronize", [](Solver& s) {
+        py::gil_scoped_release nogil;
+        s.synchronize();
+      })
+      .def("state", [](Solver& s) {
+        HostState h = s.state();
+        py::dict d;
+        d["norm"] = h.norm;
+        d["eps"] = h.eps;
+        d["last_residual"] = h.last_residual;
+        d["iter"] = h.iter;
+        d["conv_iter"] = h.conv_iter;
+        d["done"] = h.done;
+        d["fault"] = h.fault;
+        return d;
+      })
+      .def("compute_error", [](Solver& s) {
+        double g = 0, l = 0;
+        s.compute_error(&g, &l);
+        return py::make_tuple(g, l);
+      })
+      .def("gather_global", [](Solver& s) -> py::object {
+        std::vector<double> v;
+        bool root;
+        {
+          py::gil_scoped_release nogil;
+          root = s.gather_global(&v);
+        }
+        if (!root) return py::none();
+        const auto& N = s.decomposition().N;
+        return to_numpy(std::move(v), {(py::ssize_t)N[0], (py::ssize_t)N[1], (py::ssize_t)N[2]});
+      })
+      .def("local_field", [](Solver& s, int idx, bool ghosts) {
+        auto v = s.local_field(idx, ghosts);
+        const auto& sd = s.local_subdomain(idx);
+        const int g = ghosts ? 2 : 0;
+        return to_numpy(std::move(v), {(py::ssize_t)(sd.n[0] + g), (py::ssize_t)(sd.n[1] + g), (py::ssize_t)(sd.n[2] + g)});
+      }, py::arg("idx") = 0, py::arg("ghosts") = false)
+      .def("local_subdomain", [](Solver& s, int i) { return sub_dict(s.local_subdomain(i)); })
+      .def("local_layout", [](Solver& s, int i) { return layout_dict(s.local_layout(i)); })
+      .def("local_field_ptr", [](Solver& s, int i) { return reinterpret_cast<int64_t>(s.local_field_ptr(i)); })
+      .def("write_tecplot", [](Solver& s, const std::string& path, const std::string& layout) {
+        py::gil_scoped_release nogil;
+        s.write_tecplot(path, layout);
+      }, py::arg("path"), py::arg("layout") = "auto")
+      .def("save_checkpoint", [](Solver& s, const std::string& d) {
+        py::gil_scoped_release nogil;
+        s.save_checkpoint(d);
+      })
+      .def("load_checkpoint", [](Solver& s, const std::string& d) {
+        py::gil_scoped_release nogil;
+        s.load_checkpoint(d);
+      })
+      .def("inject", &Solver::inject)
+      .def("set_phase_timing", &Solver::set_phase_timing)
+      .def("phase_times", &Solver::phase_times)
+      .def_property_readonly("num_local", &Solver::num_local)
+      .def_property_readonly("is_root", &Solver::is_root)
+      .def_property_readonly("process_rank", &Solver::process_rank)
+      .def_property_readonly("interior_points", &Solver::interior_points)
+      .def_property_readonly("iterations_issued", &Solver::iterations_issued)
+      .def_property_readonly("kernel_name", &Solver::kernel_name)
+      .def_property_readonly("backend_name", [](Solver& s) { return std::string(s.backend().name()); })
+      .def_property_readonly("comm_name", [](Solver& s) { return std::string(s.comm().name()); })
+      .def_property_readonly("comm_size", [](Solver& s) { return s.comm().size(); })
+      .def_property_readonly("dims", [](Solver& s) { return s.decomposition().topo.dims; })
+      .def_property_readonly("physics", [](Solver& s) {
+        const Physics& p = s.physics();
+        py::dict d;
+        d["h"] = py::make_tuple(p.h[0], p.h[1], p.h[2]);
+        d["dt"] = p.dt;
+        d["D"] = py::make_tuple(p.D[0], p.D[1], p.D[2]);
+        return d;
+      });
+}

@@ -1,0 +1,83 @@
+// heat3d-mi355x — execution backend (HIP device or CPU host).
+//
+// The reference allocated, copied and freed device buffers and re-selected the
+// device inside every iteration (heat3D.cu:644-716).  A Backend is
+// created once: it owns the device binding, three streams (compute, comm,
+// reduce — SURVEY.md §7.2 step 6), an event pool and all allocations; the
+// solver only enqueues work.  The CPU backend runs everything synchronously
+// with OpenMP and turns stream/event calls into no-ops.
+#pragma once
+
+#include <cstddef>
+#include <memory>
+#include <string>
+
+#include "../core/common.hpp"
+#include "../kernels/kernels.hpp"
+
+namespace heat3d {
+
+enum StreamId : int { kCompute = 0, kComm = 1, kReduce = 2, kNumStreams = 3 };
+
+enum class CopyKind { H2D, D2H, D2D, H2H };
+
+typedef void* Event;
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual const char* name() const = 0;
+  virtual bool is_gpu() const = 0;
+  virtual int device() const { return -1; }
+
+  virtual void* alloc(std::size_t bytes) = 0;        // device memory (host for CPU)
+  virtual void release(void* p) = 0;
+  virtual void* alloc_host(std::size_t bytes) = 0;   // pinned host memory
+  virtual void release_host(void* p) = 0;
+  virtual void copy(void* dst, const void* src, std::size_t bytes, CopyKind k, StreamId s) = 0;
+  virtual void memset(void* dst, int v, std::size_t bytes, StreamId s) = 0;
+
+  virtual void* stream(StreamId s) = 0;  // native handle (hipStream_t) or nullptr
+  virtual Event event_create() = 0;
+  virtual void event_destroy(Event e) = 0;
+  virtual void record(Event e, StreamId s) = 0;
+  virtual void wait(StreamId s, Event e) = 0;
+  virtual bool query(Event e) = 0;
+  virtual void event_sync(Event e) = 0;
+  virtual float elapsed_ms(Event a, Event b) = 0;
+  virtual void sync(StreamId s) = 0;
+  virtual void sync_all() = 0;
+
+  // graph capture of the compute stream (forks onto the other streams via events)
+  virtual bool supports_graphs() const { return false; }
+  virtual void begin_capture() {}
+  virtual void* end_capture() { return nullptr; }  // returns executable graph
+  virtual void launch_graph(void* /*exec*/) {}
+  virtual void destroy_graph(void* /*exec*/) {}
+
+  // kernels (see kernels.hpp)
+  virtual void init_field(DType t, const InitParams& p, StreamId s) = 0;
+  virtual void stencil(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) = 0;
+  virtual void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf,
+                        StreamId s) = 0;
+  virtual void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf,
+                          StreamId s) = 0;
+  virtual void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
+                        const Layout& Ld, const Box& bd, StreamId s) = 0;
+  virtual void check_convergence(DeviceState* st, int slot, StreamId s) = 0;
+  virtual void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
+                                const int64_t gstart[3], double hy, DeviceState* st,
+                                StreamId s) = 0;
+  virtual void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k,
+                    double value, StreamId s) = 0;
+  // tracing ranges (roctx on HIP)
+  virtual void range_push(const char* /*name*/) {}
+  virtual void range_pop() {}
+};
+
+// Factory helpers.  make_hip_backend throws if no GPU is visible.
+std::unique_ptr<Backend> make_cpu_backend(int threads);
+std::unique_ptr<Backend> make_hip_backend(int device);
+int hip_device_count();  // 0 when no GPU / no driver
+
+}  // namespace heat3d

@@ -1,0 +1,785 @@
+#include "solver.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <sstream>
+#include <thread>
+
+#include "../comm/net.hpp"
+#include "../io/io.hpp"
+
+namespace heat3d {
+
+// ---------------------------------------------------------------------------
+// KernelSpec
+KernelSpec KernelSpec::parse(const std::string& s) {
+  KernelSpec k;
+  if (s.empty() || s == "auto") return k;
+  std::vector<std::string> parts;
+  std::stringstream ss(s);
+  std::string p;
+  while (std::getline(ss, p, ':')) parts.push_back(p);
+  if (parts[0] == "naive") {
+    k.kind = Naive;
+  } else if (parts[0] == "column") {
+    k.kind = Column;
+    if (parts.size() > 1) k.V = std::atoi(parts[1].c_str());
+    if (parts.size() > 2) k.R = std::atoi(parts[2].c_str());
+    if (parts.size() > 3) k.L = std::atoi(parts[3].c_str());
+  } else {
+    throw UsageError("unknown kernel '" + s + "' (auto | naive | column[:V[:R[:L]]])");
+  }
+  return k;
+}
+
+std::string KernelSpec::str() const {
+  if (kind == Naive) return "naive";
+  std::ostringstream os;
+  os << "column:" << V << ":" << R << ":" << L;
+  return os.str();
+}
+
+// ---------------------------------------------------------------------------
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<Comm> comm,
+               std::array<int, 3> dims)
+    : cfg_(cfg), be_(std::move(be)), comm_(std::move(comm)) {
+  dt_ = cfg_.dtype;
+  esize_ = dtype_size(dt_);
+  phys_ = Physics::make(cfg_.n[0], cfg_.n[1], cfg_.n[2]);
+  HEAT3D_CHECK(dims[0] * dims[1] * dims[2] == comm_->size(),
+               "process grid " << dims[0] << "x" << dims[1] << "x" << dims[2] << " does not match "
+                               << comm_->size() << " ranks");
+  dec_ = Decomposition::make(cfg_.n, dims);
+  kspec_ = KernelSpec::parse(cfg_.kernel);
+  overlap_ = cfg_.overlap;
+  if (comm_->all_local() && !be_->is_gpu()) overlap_ = cfg_.overlap;
+
+  for (int r : comm_->local_ranks()) {
+    Local l;
+    l.sd = dec_.subs[r];
+    l.L = Layout::make(l.sd.n, (int64_t)esize_);
+    for (int b = 0; b < 2; ++b) l.field[b] = be_->alloc(l.L.bytes());
+    for (int a = 0; a < 3; ++a) {
+      l.owned.lo[a] = 0;
+      l.owned.hi[a] = l.sd.n[a];
+    }
+    Decomposition::split_interior(l.sd, &l.interior, &l.shell);
+    local_.push_back(l);
+  }
+  setup_faces();
+  dstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
+  hstate_ = static_cast<DeviceState*>(be_->alloc_host(2 * sizeof(DeviceState)));
+  std::memset(hstate_, 0, 2 * sizeof(DeviceState));
+  for (auto& e : ev_) e = be_->event_create();
+}
+
+Solver::~Solver() {
+  try {
+    be_->sync_all();
+  } catch (...) {
+  }
+  if (graph_) be_->destroy_graph(graph_);
+  for (auto& e : ev_)
+    if (e) be_->event_destroy(e);
+  for (auto& l : local_) {
+    for (auto* f : l.field) be_->release(f);
+    for (auto& io : l.faces) {
+      be_->release(io.sendbuf);
+      be_->release(io.recvbuf);
+    }
+  }
+  be_->release(dstate_);
+  be_->release_host(hstate_);
+  comm_.reset();  // communicators before the device
+}
+
+bool Solver::is_root() const {
+  for (const auto& l : local_)
+    if (l.sd.rank == 0) return true;
+  return false;
+}
+
+void Solver::setup_faces() {
+  has_halo_ = false;
+  for (auto& l : local_) {
+    for (int f = 0; f < kNumFaces; ++f) {
+      const Face face = static_cast<Face>(f);
+      if (!l.sd.has_neighbor(face)) continue;
+      has_halo_ = true;
+      FaceIO io;
+      io.face = face;
+      io.peer = l.sd.neighbors[f];
+      const int a = face_axis(face), side = face_side(face);
+      for (int b = 0; b < 3; ++b) {
+        io.send_box.lo[b] = io.recv_box.lo[b] = 0;
+        io.send_box.hi[b] = io.recv_box.hi[b] = l.sd.n[b];
+      }
+      io.send_box.lo[a] = side ? l.sd.n[a] - 1 : 0;
+      io.send_box.hi[a] = io.send_box.lo[a] + 1;
+      io.recv_box.lo[a] = side ? l.sd.n[a] : -1;
+      io.recv_box.hi[a] = io.recv_box.lo[a] + 1;
+      if (comm_->all_local()) {
+        for (std::size_t q = 0; q < local_.size(); ++q)
+          if (local_[q].sd.rank == io.peer) io.peer_local = (int)q;
+        HEAT3D_CHECK(io.peer_local >= 0, "local neighbour not found");
+      } else if (a == 0) {
+        // x faces: whole planes (ghost rows and padding included) are
+        // contiguous; the neighbour across an x face has the same ny, nz and
+        // therefore the same strides.
+        io.contiguous = true;
+        const int64_t si = io.send_box.lo[0], ri = io.recv_box.lo[0];
+        io.send_off = (si + 1) * l.L.sx;
+        io.recv_off = (ri + 1) * l.L.sx;
+        io.elems = l.L.sx;
+      } else {
+        io.elems = io.send_box.volume();
+        io.sendbuf = be_->alloc(io.elems * esize_);
+        io.recvbuf = be_->alloc(io.elems * esize_);
+      }
+      l.faces.push_back(io);
+    }
+  }
+  if (!has_halo_) overlap_ = false;  // nothing to overlap with
+}
+
+InitParams Solver::init_params(const Local& l) const {
+  InitParams p;
+  p.L = l.L;
+  for (int a = 0; a < 3; ++a) {
+    p.gstart[a] = l.sd.gstart[a];
+    p.N[a] = dec_.N[a];
+    p.h[a] = phys_.h[a];
+  }
+  return p;
+}
+
+void Solver::ev_record(int id, StreamId s) {
+  be_->record(ev_[id], s);
+  ev_valid_[id] = true;
+}
+
+void Solver::ev_wait(StreamId s, int id) {
+  if (ev_valid_[id]) be_->wait(s, ev_[id]);
+}
+
+void Solver::initialize() {
+  be_->sync_all();
+  if (graph_) {
+    be_->destroy_graph(graph_);
+    graph_ = nullptr;
+  }
+  for (auto& l : local_) {
+    InitParams p = init_params(l);
+    for (int b = 0; b < 2; ++b) {
+      p.field = l.field[b];
+      be_->init_field(dt_, p, kCompute);
+    }
+  }
+  DeviceState hs;
+  std::memset(&hs, 0, sizeof(hs));
+  hs.residual[0] = hs.residual[1] = kResidualInitBits;
+  hs.norm = 1.0;  // heat3D.cu:323-324 (norm = 1 until iteration 0 sets it)
+  hs.eps = cfg_.eps;
+  hs.iter = 0;
+  hs.conv_iter = -1;
+  hs.hist_cap = 1024;
+  std::memcpy(hstate_, &hs, sizeof(hs));
+  be_->copy(dstate_, hstate_, sizeof(DeviceState), CopyKind::H2D, kCompute);
+  be_->sync(kCompute);
+  issued_ = 0;
+  if (!cfg_.restart.empty()) load_checkpoint(cfg_.restart);
+  // make every pipeline event valid (complete) before the first iteration
+  for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
+  for (int p = 0; p < 2; ++p) {
+    ev_record(EV_INT + p, kCompute);
+    ev_record(EV_BND + p, kComm);
+    ev_record(EV_CHK + p, kReduce);
+  }
+  be_->sync_all();
+  comm_->barrier(*be_);
+}
+
+// --- one iteration -----------------------------------------------------------
+void Solver::enqueue_halo(int p) {
+  const StreamId s = overlap_ ? kComm : kCompute;
+  be_->range_push("halo");
+  if (comm_->all_local()) {
+    for (auto& l : local_)
+      for (auto& io : l.faces) {
+        const Local& nb = local_[io.peer_local];
+        const Box* src = nullptr;
+        for (auto& nio : nb.faces)
+          if (nio.face == opposite(io.face)) src = &nio.send_box;
+        HEAT3D_CHECK(src, "opposite face missing");
+        be_->copy_box(dt_, nb.field[p], nb.L, *src, l.field[p], l.L, io.recv_box, s);
+      }
+  } else {
+    std::vector<Transfer> xs;
+    for (auto& l : local_) {
+      char* base = static_cast<char*>(l.field[p]);
+      for (auto& io : l.faces) {
+        if (!io.contiguous) be_->pack_box(dt_, l.field[p], l.L, io.send_box, io.sendbuf, s);
+        Transfer snd, rcv;
+        snd.src_rank = l.sd.rank;
+        snd.dst_rank = io.peer;
+        snd.src = io.contiguous ? base + io.send_off * esize_ : io.sendbuf;
+        snd.bytes = io.elems * esize_;
+        rcv.src_rank = io.peer;
+        rcv.dst_rank = l.sd.rank;
+        rcv.dst = io.contiguous ? base + io.recv_off * esize_ : io.recvbuf;
+        rcv.bytes = io.elems * esize_;
+        xs.push_back(snd);
+        xs.push_back(rcv);
+      }
+    }
+    comm_->exchange(xs, *be_, s);
+    for (auto& l : local_)
+      for (auto& io : l.faces)
+        if (!io.contiguous) be_->unpack_box(dt_, l.field[p], l.L, io.recv_box, io.recvbuf, s);
+  }
+  be_->range_pop();
+}
+
+void Solver::enqueue_iteration(int p) {
+  auto params = [&](Local& l, const Box& b) {
+    StencilParams sp;
+    sp.in = l.field[p];
+    sp.out = l.field[p ^ 1];
+    sp.L = l.L;
+    sp.box = b;
+    for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+    sp.state = dstate_;
+    sp.slot = p;
+    return sp;
+  };
+  // [A] interior sweep on the compute stream
+  ev_wait(kCompute, EV_CHK + p);  // convergence check of iteration t-2 (flag + slot reset)
+  if (overlap_) {
+    ev_wait(kCompute, EV_BND + (p ^ 1));  // shell of t-1 written (and read) before we overwrite
+    be_->range_push("interior");
+    for (auto& l : local_) be_->stencil(dt_, params(l, l.interior), kspec_, kCompute);
+    be_->range_pop();
+    ev_record(EV_INT + p, kCompute);
+    // [B] halo exchange + shell on the comm stream
+    ev_wait(kComm, EV_INT + (p ^ 1));  // interior of t-1 done (RAW on layer 1, WAR on shell)
+    ev_wait(kComm, EV_CHK + p);
+    enqueue_halo(p);
+    be_->range_push("shell");
+    for (auto& l : local_)
+      for (const Box& b : l.shell) be_->stencil(dt_, params(l, b), kspec_, kComm);
+    be_->range_pop();
+    ev_record(EV_BND + p, kComm);
+  } else {
+    if (has_halo_) enqueue_halo(p);
+    be_->range_push("sweep");
+    for (auto& l : local_) be_->stencil(dt_, params(l, l.owned), kspec_, kCompute);
+    be_->range_pop();
+    ev_record(EV_INT + p, kCompute);
+  }
+  // [C] global residual + convergence check on the reduce stream
+  ev_wait(kReduce, EV_INT + p);
+  if (overlap_) ev_wait(kReduce, EV_BND + p);
+  if (!comm_->all_local() && comm_->size() > 1)
+    comm_->allreduce(&dstate_->residual[p], 1, RedType::U64, RedOp::Max, *be_, kReduce);
+  be_->check_convergence(dstate_, p, kReduce);
+  ev_record(EV_CHK + p, kReduce);
+}
+
+void Solver::build_graph() {
+  const int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
+  graph_parity_ = (int)(issued_ & 1);
+  bool saved[EV_COUNT];
+  std::memcpy(saved, ev_valid_, sizeof(saved));
+  try {
+    be_->begin_capture();
+    capturing_ = true;
+    for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
+    ev_record(EV_FORK, kCompute);
+    be_->wait(kComm, ev_[EV_FORK]);
+    be_->wait(kReduce, ev_[EV_FORK]);
+    for (int i = 0; i < G; ++i) enqueue_iteration((graph_parity_ + i) & 1);
+    ev_record(EV_JCOMM, kComm);
+    ev_record(EV_JRED, kReduce);
+    be_->wait(kCompute, ev_[EV_JCOMM]);
+    be_->wait(kCompute, ev_[EV_JRED]);
+    graph_ = be_->end_capture();
+    capturing_ = false;
+    graph_iters_ = G;
+  } catch (const std::exception& e) {
+    if (capturing_) {
+      try {
+        be_->end_capture();
+      } catch (...) {
+      }
+      capturing_ = false;
+    }
+    graph_ = nullptr;
+    graph_failed_ = true;
+    if (!cfg_.quiet && is_root())
+      std::fprintf(stderr, "heat3d: hipGraph capture failed (%s); running eagerly\n", e.what());
+  }
+  std::memcpy(ev_valid_, saved, sizeof(saved));
+}
+
+void Solver::run_chunk(int64_t n) {
+  const bool graphs = cfg_.use_graph && be_->supports_graphs() && comm_->capturable() &&
+                      !graph_failed_ && !phase_timing_;
+  while (n > 0) {
+    const int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
+    if (graphs && n >= G && (graph_ == nullptr || (int)(issued_ & 1) == graph_parity_)) {
+      if (!graph_) build_graph();
+      if (graph_ && (int)(issued_ & 1) == graph_parity_) {
+        be_->launch_graph(graph_);
+        issued_ += graph_iters_;
+        n -= graph_iters_;
+        // the graph joined every stream into compute: re-fork for eager work
+        for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
+        ev_record(EV_FORK, kCompute);
+        be_->wait(kComm, ev_[EV_FORK]);
+        be_->wait(kReduce, ev_[EV_FORK]);
+        continue;
+      }
+    }
+    if (phase_timing_) {
+      ev_record(EV_T0, kCompute);
+    }
+    enqueue_iteration((int)(issued_ & 1));
+    if (phase_timing_) {
+      ev_record(EV_T1, kReduce);
+      be_->event_sync(ev_[EV_T1]);
+      double ms = be_->elapsed_ms(ev_[EV_T0], ev_[EV_T1]);
+      if (phase_acc_.empty()) phase_acc_.push_back({"iteration_ms", 0.0});
+      phase_acc_[0].second += ms;
+    }
+    ++issued_;
+    --n;
+  }
+}
+
+void Solver::step(int64_t n) { run_chunk(n); }
+
+void Solver::synchronize() {
+  be_->sync_all();
+  comm_->check_async_error();
+}
+
+void Solver::poll_enqueue(StreamId s) { (void)s; }
+
+HostState Solver::state() {
+  be_->sync_all();
+  be_->copy(hstate_, dstate_, sizeof(DeviceState), CopyKind::D2H, kCompute);
+  be_->sync(kCompute);
+  HostState h;
+  h.norm = hstate_->norm;
+  h.eps = hstate_->eps;
+  h.last_residual = hstate_->last_residual;
+  h.error_sum = hstate_->error_sum;
+  h.error_count = hstate_->error_count;
+  h.iter = hstate_->iter;
+  h.conv_iter = hstate_->conv_iter;
+  h.done = hstate_->done;
+  h.fault = hstate_->fault;
+  return h;
+}
+
+RunResult Solver::run() {
+  RunResult R;
+  comm_->barrier(*be_);
+  be_->sync_all();
+  const double t0 = now_s();
+  const int64_t K = std::max(1, cfg_.check_every);
+  const std::size_t poll_bytes = cfg_.verbose > 0 ? sizeof(DeviceState) : offsetof(DeviceState, hist);
+  int pslot = 0;
+  bool have_prev = false, stop = false;
+  int64_t next_ckpt = cfg_.checkpoint_every > 0 ? issued_ + cfg_.checkpoint_every : -1;
+  int64_t printed = issued_;
+  const double watchdog = std::getenv("HEAT3D_WATCHDOG_S") ? std::atof(std::getenv("HEAT3D_WATCHDOG_S")) : 900.0;
+  while (issued_ < cfg_.iter_max && !stop) {
+    int64_t n = std::min(K, cfg_.iter_max - issued_);
+    if (next_ckpt > 0) n = std::min(n, next_ckpt - issued_);
+    run_chunk(n);
+    // pinned copy of the device convergence state, polled one chunk later
+    be_->copy(&hstate_[pslot], dstate_, poll_bytes, CopyKind::D2H, kReduce);
+    ev_record(EV_POLL + pslot, kReduce);
+    if (have_prev) {
+      const int q = pslot ^ 1;
+      const double tw = now_s();
+      while (!be_->query(ev_[EV_POLL + q])) {
+        comm_->check_async_error();
+        if (now_s() - tw > watchdog) {
+          comm_->abort();
+          HEAT3D_THROW("watchdog: no progress for " << watchdog << " s (peer failure?)");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+      const DeviceState& hs = hstate_[q];
+      if (cfg_.verbose > 0 && is_root()) {
+        for (int64_t it = printed; it < hs.iter; ++it)
+          if (it % cfg_.verbose == 0 && it >= hs.iter - hs.hist_cap)
+            std::printf("iteration %lld residual %.6e\n", (long long)it, hs.hist[it % hs.hist_cap]);
+        printed = hs.iter;
+      }
+      if (hs.done) stop = true;
+    }
+    have_prev = true;
+    pslot ^= 1;
+    if (next_ckpt > 0 && issued_ >= next_ckpt && !stop) {
+      HostState hs = state();
+      if (!hs.done) save_checkpoint(cfg_.checkpoint_dir.empty() ? "checkpoint" : cfg_.checkpoint_dir);
+      next_ckpt = issued_ + cfg_.checkpoint_every;
+    }
+  }
+  be_->sync_all();
+  comm_->check_async_error();
+  const double t1 = now_s();
+  HostState hs = state();
+  if (cfg_.verbose > 0 && is_root()) {
+    be_->copy(hstate_, dstate_, sizeof(DeviceState), CopyKind::D2H, kCompute);
+    be_->sync(kCompute);
+    for (int64_t it = printed; it < hs.iter; ++it)
+      if (it % cfg_.verbose == 0 && it >= hs.iter - hstate_->hist_cap)
+        std::printf("iteration %lld residual %.6e\n", (long long)it, hstate_->hist[it % hstate_->hist_cap]);
+  }
+  R.seconds = t1 - t0;
+  R.fault = hs.fault != 0;
+  R.converged = hs.done && !hs.fault;
+  R.conv_iter = hs.conv_iter;
+  R.issued = issued_;
+  R.iterations = hs.done ? hs.conv_iter + 1 : issued_;
+  R.norm = hs.norm;
+  R.last_residual = hs.last_residual;
+  // the final field is T^{iterations}: point the "current" parity at it
+  if (hs.done) issued_ = R.iterations;
+  R.glups = R.seconds > 0 ? (double)interior_points() * (double)R.issued / R.seconds / 1e9 : 0.0;
+  return R;
+}
+
+void Solver::compute_error(double* global_mean, double* local_mean) {
+  be_->sync_all();
+  const int p = (int)(issued_ & 1);
+  const std::size_t off = offsetof(DeviceState, error_sum);
+  char* base = reinterpret_cast<char*>(dstate_);
+  be_->memset(base + off, 0, 2 * sizeof(double), kCompute);
+  for (std::size_t i = 0; i < local_.size(); ++i) {
+    auto& l = local_[i];
+    be_->error_accumulate(dt_, l.field[p], l.L, l.owned, l.sd.gstart, phys_.h[1], dstate_, kCompute);
+    if (i == 0) {
+      double e[2];
+      be_->copy(e, base + off, sizeof(e), CopyKind::D2H, kCompute);
+      be_->sync(kCompute);
+      if (local_mean) *local_mean = e[1] > 0 ? e[0] / e[1] : 0.0;
+    }
+  }
+  be_->sync(kCompute);
+  if (!comm_->all_local() && comm_->size() > 1) {
+    comm_->allreduce(base + off, 2, RedType::F64, RedOp::Sum, *be_, kCompute);
+  }
+  double e[2];
+  be_->copy(e, base + off, sizeof(e), CopyKind::D2H, kCompute);
+  be_->sync(kCompute);
+  if (global_mean) *global_mean = e[1] > 0 ? e[0] / e[1] : 0.0;
+}
+
+std::vector<double> Solver::local_field(int idx, bool with_ghosts) {
+  be_->sync_all();
+  auto& l = local_.at(idx);
+  Box b;
+  for (int a = 0; a < 3; ++a) {
+    b.lo[a] = with_ghosts ? -1 : 0;
+    b.hi[a] = l.sd.n[a] + (with_ghosts ? 1 : 0);
+  }
+  const std::size_t bytes = b.volume() * esize_;
+  void* dbuf = be_->alloc(bytes);
+  be_->pack_box(dt_, l.field[issued_ & 1], l.L, b, dbuf, kCompute);
+  std::vector<char> h(bytes);
+  be_->copy(h.data(), dbuf, bytes, CopyKind::D2H, kCompute);
+  be_->sync(kCompute);
+  be_->release(dbuf);
+  std::vector<double> out(b.volume());
+  for (std::size_t i = 0; i < out.size(); ++i)
+    out[i] = dt_ == DType::F64 ? reinterpret_cast<double*>(h.data())[i]
+                               : (double)reinterpret_cast<float*>(h.data())[i];
+  return out;
+}
+
+bool Solver::gather_global(std::vector<double>* out) {
+  be_->sync_all();
+  const int P = comm_->size();
+  const bool root = is_root();
+  const int p = (int)(issued_ & 1);
+  const int64_t* N = dec_.N;
+  if (root) out->assign((std::size_t)(N[0] * N[1] * N[2]), 0.0);
+  int64_t maxvol = 0;
+  for (const auto& s : dec_.subs) maxvol = std::max(maxvol, s.extended_global().volume());
+  void* stage = be_->alloc(maxvol * esize_);
+  std::vector<char> host(maxvol * esize_);
+  auto scatter = [&](const Box& g) {
+    const int64_t ey = g.extent(1), ez = g.extent(2);
+    for (int64_t i = 0; i < g.extent(0); ++i)
+      for (int64_t j = 0; j < ey; ++j) {
+        double* dst = out->data() + ((g.lo[0] + i) * N[1] + (g.lo[1] + j)) * N[2] + g.lo[2];
+        const int64_t o = (i * ey + j) * ez;
+        if (dt_ == DType::F64) std::memcpy(dst, reinterpret_cast<double*>(host.data()) + o, ez * 8);
+        else
+          for (int64_t k = 0; k < ez; ++k) dst[k] = reinterpret_cast<float*>(host.data())[o + k];
+      }
+  };
+  for (int r = 0; r < P; ++r) {
+    const Subdomain& s = dec_.subs[r];
+    const Box g = s.extended_global();
+    const std::size_t bytes = g.volume() * esize_;
+    int li = -1;
+    for (std::size_t q = 0; q < local_.size(); ++q)
+      if (local_[q].sd.rank == r) li = (int)q;
+    if (li >= 0) {
+      Local& l = local_[li];
+      Box lb = g;
+      for (int a = 0; a < 3; ++a) {
+        lb.lo[a] -= s.gstart[a];
+        lb.hi[a] -= s.gstart[a];
+      }
+      be_->pack_box(dt_, l.field[p], l.L, lb, stage, kCompute);
+      if (root) {
+        be_->copy(host.data(), stage, bytes, CopyKind::D2H, kCompute);
+        be_->sync(kCompute);
+        scatter(g);
+      } else {
+        if (comm_->device_buffers()) {
+          comm_->send(stage, bytes, 0, *be_, kCompute);
+          be_->sync(kCompute);
+        } else {
+          be_->sync(kCompute);
+          comm_->send(stage, bytes, 0, *be_, kCompute);
+        }
+      }
+    } else if (root) {
+      comm_->recv(stage, bytes, r, *be_, kCompute);
+      be_->copy(host.data(), stage, bytes, CopyKind::D2H, kCompute);
+      be_->sync(kCompute);
+      scatter(g);
+    }
+  }
+  be_->sync_all();
+  be_->release(stage);
+  return root;
+}
+
+void Solver::write_tecplot(const std::string& path, const std::string& layout_req) {
+  std::vector<double> g;
+  const bool root = gather_global(&g);
+  if (!root) return;
+  const int P = comm_->size();
+  std::vector<io::Zone> zones;
+  bool ref_legal = true;
+  for (int a = 0; a < 3; ++a) ref_legal &= (dec_.N[a] - 1) % dec_.topo.dims[a] == 0;
+  std::string layout = layout_req;
+  if (layout == "auto") layout = ref_legal ? "ref" : "owned";
+  if (layout == "ref" && !ref_legal)
+    HEAT3D_THROW("--tecplot-layout ref needs (N-1) % dims == 0 on every axis (heat3D.cu:375-380)");
+  for (int r = 0; r < P; ++r) {
+    io::Zone z;
+    z.rank = r;
+    z.title = cfg_.compat ? 0 : r;  // the reference always printed rank 0's id (heat3D.cu:1148)
+    if (layout == "ref") {
+      // reference chunks: c = (N-1)/dims + 1 points, sharing one plane with
+      // each neighbour (heat3D.cu:385-389, 1135)
+      auto c = dec_.topo.coords(r);
+      for (int a = 0; a < 3; ++a) {
+        const int64_t ch = (dec_.N[a] - 1) / dec_.topo.dims[a] + 1;
+        z.lo[a] = c[a] * (ch - 1);
+        z.hi[a] = z.lo[a] + ch;
+      }
+    } else {
+      Box b = dec_.subs[r].extended_global();
+      for (int a = 0; a < 3; ++a) {
+        z.lo[a] = b.lo[a];
+        z.hi[a] = b.hi[a];
+      }
+    }
+    zones.push_back(z);
+  }
+  io::write_tecplot(path, g, dec_.N, phys_.h, zones, P > 1);
+}
+
+void Solver::save_checkpoint(const std::string& dir) {
+  be_->sync_all();
+  HostState hs = state();
+  io::make_dirs(dir);
+  const std::string raw = dir + "/field.raw";
+  const int p = (int)(issued_ & 1);
+  const int64_t* N = dec_.N;
+  {
+    int fd = io::open_raw(raw, true);
+    for (auto& l : local_) {
+      Box g = l.sd.extended_global();
+      Box lb = g;
+      for (int a = 0; a < 3; ++a) {
+        lb.lo[a] -= l.sd.gstart[a];
+        lb.hi[a] -= l.sd.gstart[a];
+      }
+      const std::size_t bytes = g.volume() * esize_;
+      void* stage = be_->alloc(bytes);
+      be_->pack_box(dt_, l.field[p], l.L, lb, stage, kCompute);
+      std::vector<char> host(bytes);
+      be_->copy(host.data(), stage, bytes, CopyKind::D2H, kCompute);
+      be_->sync(kCompute);
+      be_->release(stage);
+      const int64_t ey = g.extent(1), ez = g.extent(2);
+      for (int64_t i = 0; i < g.extent(0); ++i)
+        for (int64_t j = 0; j < ey; ++j) {
+          const int64_t off = (((g.lo[0] + i) * N[1] + (g.lo[1] + j)) * N[2] + g.lo[2]) * esize_;
+          io::pwrite_all(fd, host.data() + (i * ey + j) * ez * esize_, ez * esize_, off);
+        }
+    }
+    io::close_raw(fd);
+  }
+  comm_->barrier(*be_);
+  if (is_root()) {
+    io::Json j;
+    j.set("format", std::string("heat3d-checkpoint-v1"));
+    j.set_raw("N", "[" + std::to_string(N[0]) + ", " + std::to_string(N[1]) + ", " + std::to_string(N[2]) + "]");
+    j.set("dtype", std::string(dtype_name(dt_)));
+    j.set("iteration", (int64_t)issued_);
+    j.set("norm", hs.norm);
+    j.set("eps", hs.eps);
+    j.set("last_residual", hs.last_residual);
+    j.set_raw("dims", "[" + std::to_string(dec_.topo.dims[0]) + ", " + std::to_string(dec_.topo.dims[1]) +
+                          ", " + std::to_string(dec_.topo.dims[2]) + "]");
+    j.set("layout", std::string("global z-fastest, N0*N1*N2 values"));
+    io::write_file_atomic(dir + "/meta.json", j.dump() + "\n");
+  }
+  comm_->barrier(*be_);
+}
+
+void Solver::load_checkpoint(const std::string& dir) {
+  auto meta = io::Json::parse_flat(io::read_file(dir + "/meta.json"));
+  HEAT3D_CHECK(meta["format"] == "heat3d-checkpoint-v1", "not a heat3d checkpoint: " << dir);
+  const std::string Nexp = "[" + std::to_string(dec_.N[0]) + ", " + std::to_string(dec_.N[1]) + ", " +
+                           std::to_string(dec_.N[2]) + "]";
+  HEAT3D_CHECK(meta["N"] == Nexp, "checkpoint grid " << meta["N"] << " != run grid " << Nexp);
+  HEAT3D_CHECK(meta["dtype"] == dtype_name(dt_), "checkpoint dtype " << meta["dtype"] << " != " << dtype_name(dt_));
+  const int64_t it = std::atoll(meta["iteration"].c_str());
+  const double norm = std::atof(meta["norm"].c_str());
+  const int64_t* N = dec_.N;
+  int fd = io::open_raw(dir + "/field.raw", false);
+  for (auto& l : local_) {
+    const int64_t ez = l.sd.n[2] + 2;
+    Box lb;
+    for (int a = 0; a < 3; ++a) {
+      lb.lo[a] = -1;
+      lb.hi[a] = l.sd.n[a] + 1;
+    }
+    const int64_t ey = lb.extent(1);
+    std::vector<char> host(lb.volume() * esize_);
+    for (int64_t i = 0; i < lb.extent(0); ++i)
+      for (int64_t j = 0; j < ey; ++j) {
+        const int64_t gi = l.sd.gstart[0] - 1 + i, gj = l.sd.gstart[1] - 1 + j, gk = l.sd.gstart[2] - 1;
+        const int64_t off = ((gi * N[1] + gj) * N[2] + gk) * esize_;
+        io::pread_all(fd, host.data() + (i * ey + j) * ez * esize_, ez * esize_, off);
+      }
+    void* stage = be_->alloc(host.size());
+    be_->copy(stage, host.data(), host.size(), CopyKind::H2D, kCompute);
+    for (int b = 0; b < 2; ++b) be_->unpack_box(dt_, l.field[b], l.L, lb, stage, kCompute);
+    be_->sync(kCompute);
+    be_->release(stage);
+  }
+  io::close_raw(fd);
+  be_->copy(hstate_, dstate_, sizeof(DeviceState), CopyKind::D2H, kCompute);
+  be_->sync(kCompute);
+  hstate_->iter = it;
+  hstate_->norm = norm;
+  hstate_->done = 0;
+  hstate_->conv_iter = -1;
+  hstate_->residual[0] = hstate_->residual[1] = kResidualInitBits;
+  be_->copy(dstate_, hstate_, sizeof(DeviceState), CopyKind::H2D, kCompute);
+  be_->sync(kCompute);
+  issued_ = it;
+}
+
+std::vector<std::pair<std::string, double>> Solver::phase_times() { return phase_acc_; }
+
+void Solver::inject(int idx, int64_t i, int64_t j, int64_t k, double value) {
+  be_->sync_all();
+  auto& l = local_.at(idx);
+  be_->poke(dt_, l.field[issued_ & 1], l.L, i, j, k, value, kCompute);
+  be_->sync(kCompute);
+}
+
+// ---------------------------------------------------------------------------
+static int env_int(const char* a, const char* b, int dflt) {
+  const char* v = std::getenv(a);
+  if ((!v || !*v) && b) v = std::getenv(b);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+std::unique_ptr<Solver> make_solver_from_env(const Config& cfg) {
+  const int rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", env_int("PMI_RANK", nullptr, 0));
+  const int size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", env_int("PMI_SIZE", nullptr, 1));
+  const int local_rank = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", env_int("MPI_LOCALRANKID", nullptr, rank));
+  const char* ma = std::getenv("MASTER_ADDR");
+  const std::string master = ma && *ma ? ma : "127.0.0.1";
+  // The native CLI never shares a process with torch, but torchrun's agent owns
+  // MASTER_PORT; bootstrap on MASTER_PORT + 1 unless told otherwise.
+  const int bport = env_int("HEAT3D_BOOTSTRAP_PORT", nullptr, env_int("MASTER_PORT", nullptr, 29500) + 1);
+
+  BackendKind bk = cfg.backend;
+  if (bk == BackendKind::Auto) bk = hip_device_count() > 0 ? BackendKind::Hip : BackendKind::Cpu;
+  CommKind ck = cfg.comm;
+  if (ck == CommKind::Auto) {
+    if (cfg.virtual_ranks > 1) ck = CommKind::Local;
+    else if (size > 1) ck = bk == BackendKind::Hip ? CommKind::Rccl : CommKind::Socket;
+    else ck = CommKind::None;
+  }
+  int device = cfg.device >= 0 ? cfg.device : 0;
+  if (bk == BackendKind::Hip && cfg.device < 0) {
+    const int n = hip_device_count();
+    device = n > 0 ? local_rank % n : 0;
+  }
+  std::unique_ptr<Backend> be = bk == BackendKind::Hip ? make_hip_backend(device) : make_cpu_backend(cfg.cpu_threads);
+  std::unique_ptr<Comm> comm;
+  int nranks = 1;
+  switch (ck) {
+    case CommKind::None:
+    case CommKind::Auto:
+      HEAT3D_CHECK(size == 1, "WORLD_SIZE=" << size << " needs --comm rccl or socket");
+      comm = make_local_comm(1);
+      nranks = 1;
+      break;
+    case CommKind::Local:
+      HEAT3D_CHECK(size == 1, "--comm local runs in a single process");
+      nranks = cfg.virtual_ranks;
+      comm = make_local_comm(nranks);
+      break;
+    case CommKind::Socket: {
+      net::Bootstrap boot(rank, size, master, bport);
+      comm = make_socket_comm(rank, size, boot);
+      nranks = size;
+      break;
+    }
+    case CommKind::Rccl: {
+      HEAT3D_CHECK(bk == BackendKind::Hip, "RCCL needs the HIP backend");
+      net::Bootstrap boot(rank, size, master, bport);
+      std::string uid = rank == 0 ? rccl_unique_id() : std::string();
+      auto all = boot.allgather(uid);
+      comm = make_rccl_comm(rank, size, all[0], device);
+      nranks = size;
+      break;
+    }
+  }
+  std::array<int, 3> fixed = {0, 0, 0};
+  if (cfg.decomp[0] > 0) fixed = cfg.decomp;
+  std::array<int, 3> dims = dims_create(nranks, fixed);
+  return std::unique_ptr<Solver>(new Solver(cfg, std::move(be), std::move(comm), dims));
+}
+
+}  // namespace heat3d

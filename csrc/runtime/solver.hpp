@@ -1,0 +1,180 @@
+// heat3d-mi355x — the time-stepping engine.
+//
+// Reference call stack being replaced (heat3D.cu:541-1073):
+// per iteration a full-volume host copy T0 = T, host face packing, 6 MPI
+// Isends, a per-iteration GPU alloc/copy/launch/copy/free, blocking receives,
+// host face/edge/corner updates, a host residual scan and a blocking
+// MPI_Iallreduce of a break flag.
+//
+// Here one iteration t (parity p = t & 1, in = field[p], out = field[p^1]) is
+//   compute stream : interior stencil (+ fused residual)            [A]
+//   comm stream    : pack y/z faces -> exchange -> unpack -> shell stencils [B]
+//   reduce stream  : allreduce(max residual) -> convergence check    [C]
+// with A(t) || B(t), C(t) || A(t+1), B(t+1).  Kernels of iteration t+2 wait
+// for C(t) and read its device flag: once converged they are no-ops, which
+// leaves T^{t_conv+1} intact in field[(t_conv+1)&1].  The host polls a pinned
+// copy of the flag every `check_every` iterations and never blocks the GPU
+// pipeline per iteration (the reference synchronised every step,
+// heat3D.cu:1062-1063).  Chunks of an even number of iterations are captured
+// once into a hipGraph and replayed.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../comm/comm.hpp"
+#include "../core/config.hpp"
+#include "../core/decomp.hpp"
+#include "backend.hpp"
+
+namespace heat3d {
+
+struct RunResult {
+  bool converged = false;
+  bool fault = false;
+  int64_t conv_iter = -1;    // 0-based iteration at which the criterion was met
+  int64_t iterations = 0;    // iterations whose result is in the final field
+  int64_t issued = 0;        // iterations enqueued (>= iterations when converged)
+  double seconds = 0.0;      // wall time of the time loop (MPI_Wtime analogue)
+  double norm = 1.0;
+  double last_residual = 0.0;
+  double error_mean = 0.0;   // global mean |T - y| over interior points
+  double error_local = 0.0;  // this process's first subdomain (reference prints rank-0 local)
+  double glups = 0.0;        // updated interior points x iterations / s (whole job)
+};
+
+struct HostState {
+  double norm, eps, last_residual, error_sum, error_count;
+  int64_t iter, conv_iter;
+  int done, fault;
+};
+
+class Solver {
+ public:
+  // `process_rank` is the rank hosted by this process (ignored for LocalComm,
+  // which hosts every rank).
+  Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<Comm> comm,
+         std::array<int, 3> dims);
+  ~Solver();
+  Solver(const Solver&) = delete;
+  Solver& operator=(const Solver&) = delete;
+
+  const Config& config() const { return cfg_; }
+  const Decomposition& decomposition() const { return dec_; }
+  const Physics& physics() const { return phys_; }
+  Backend& backend() { return *be_; }
+  Comm& comm() { return *comm_; }
+  int process_rank() const { return local_.empty() ? 0 : local_[0].sd.rank; }
+  bool is_root() const;
+  int64_t interior_points() const { return (dec_.N[0] - 2) * (dec_.N[1] - 2) * (dec_.N[2] - 2); }
+  std::string kernel_name() const { return kspec_.str(); }
+
+  // (Re)initialise fields: analytic IC/BC (heat3D.cu:408-453) or restart.
+  void initialize();
+  // Full solve: iterate until converged or iter_max (heat3D.cu:541-1073).
+  RunResult run();
+  // Enqueue exactly n iterations without host polling (benchmarks); async.
+  void step(int64_t n);
+  void synchronize();
+  HostState state();
+  int64_t iterations_issued() const { return issued_; }
+
+  // Error vs analytic steady state (heat3D.cu:1093-1106, with a true global
+  // mean instead of rank-0's local value).  Uses the current field.
+  void compute_error(double* global_mean, double* local_mean);
+
+  // Field access.  gather_global fills `out` (N0*N1*N2 values as double,
+  // z fastest) on the root process only; returns false elsewhere.
+  bool gather_global(std::vector<double>* out);
+  // Local subdomain (index into local_ranks()) owned+ghost values as double.
+  std::vector<double> local_field(int local_idx, bool with_ghosts);
+  int num_local() const { return (int)local_.size(); }
+  const Subdomain& local_subdomain(int i) const { return local_[i].sd; }
+  const Layout& local_layout(int i) const { return local_[i].L; }
+  // current field buffer of a local subdomain (device pointer on HIP)
+  void* local_field_ptr(int i) { return local_[i].field[issued_ & 1]; }
+
+  // Output / checkpoint.
+  void write_tecplot(const std::string& path, const std::string& layout);
+  void save_checkpoint(const std::string& dir);
+  void load_checkpoint(const std::string& dir);
+
+  // Per-phase timing (ms, averaged over timed iterations) when enabled.
+  void set_phase_timing(bool on) { phase_timing_ = on; }
+  std::vector<std::pair<std::string, double>> phase_times();
+
+  // Fault injection for tests: write `value` into a local owned point.
+  void inject(int local_idx, int64_t i, int64_t j, int64_t k, double value);
+
+ private:
+  struct FaceIO {
+    Face face;
+    int peer;
+    Box send_box, recv_box;     // local coords
+    bool contiguous = false;    // x faces: whole planes sent in place
+    int64_t send_off = 0, recv_off = 0, elems = 0;
+    void* sendbuf = nullptr;    // staging for packed faces
+    void* recvbuf = nullptr;
+    int peer_local = -1;        // LocalComm: index of the neighbour in local_
+  };
+  struct Local {
+    Subdomain sd;
+    Layout L;
+    void* field[2] = {nullptr, nullptr};
+    Box owned, interior;
+    std::vector<Box> shell;
+    std::vector<FaceIO> faces;
+  };
+
+  void setup_faces();
+  void enqueue_iteration(int p);
+  void enqueue_halo(int p);
+  void poll_enqueue(StreamId s);
+  void ev_record(int id, StreamId s);
+  void ev_wait(StreamId s, int id);
+  void run_chunk(int64_t n);
+  void build_graph();
+  InitParams init_params(const Local& l) const;
+
+  Config cfg_;
+  std::unique_ptr<Backend> be_;
+  std::unique_ptr<Comm> comm_;
+  Decomposition dec_;
+  Physics phys_;
+  KernelSpec kspec_;
+  std::vector<Local> local_;
+  bool has_halo_ = false;  // any face with a neighbour on any local subdomain
+  bool overlap_ = true;
+  DType dt_;
+  std::size_t esize_;
+
+  DeviceState* dstate_ = nullptr;   // device
+  DeviceState* hstate_ = nullptr;   // pinned host mirror
+  int64_t issued_ = 0;              // iterations enqueued so far (absolute index)
+
+  // events: 0..1 int[p], 2..3 bnd[p], 4..5 check[p], 6 fork, 7 join comm, 8 join red, 9..10 poll
+  enum { EV_INT = 0, EV_BND = 2, EV_CHK = 4, EV_FORK = 6, EV_JCOMM = 7, EV_JRED = 8, EV_POLL = 9,
+         EV_T0 = 11, EV_T1 = 12, EV_COUNT = 16 };
+  Event ev_[EV_COUNT] = {};
+  bool ev_valid_[EV_COUNT] = {};
+  bool capturing_ = false;
+
+  void* graph_ = nullptr;
+  int graph_iters_ = 0;
+  int graph_parity_ = 0;
+  bool graph_failed_ = false;
+
+  bool phase_timing_ = false;
+  std::vector<std::pair<std::string, double>> phase_acc_;
+};
+
+// Build a Solver for a parsed command line in this process: chooses backend,
+// comm (RCCL / socket via env bootstrap, LocalComm for --virtual-ranks),
+// decomposition.  Environment: RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/
+// MASTER_PORT (torchrun / mpirun style).
+std::unique_ptr<Solver> make_solver_from_env(const Config& cfg);
+
+}  // namespace heat3d

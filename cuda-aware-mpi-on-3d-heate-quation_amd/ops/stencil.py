@@ -1,0 +1,132 @@
+"""Kernel-level ops on torch tensors.
+
+The padded field layout of the native engine (csrc/kernels/layout.hpp: owned
+block + one-cell ghost shell, z fastest, rows padded so the first owned z
+point is 128-byte aligned) is allocated as a flat torch tensor; ``PaddedField``
+exposes strided views of it.  ``ftcs_step`` launches the hand-written gfx950
+kernel on torch's current HIP stream (or the OpenMP kernel for CPU tensors);
+``ftcs_reference`` is the plain-PyTorch oracle with the reference's
+expression order (heat3D.cu:128-131).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from .._native import native
+
+_DT = {torch.float64: "fp64", torch.float32: "fp32"}
+
+
+class PaddedField:
+    """One subdomain field in the native padded layout."""
+
+    def __init__(self, n: Sequence[int], dtype=torch.float64, device="cpu"):
+        if dtype not in _DT:
+            raise TypeError(f"unsupported dtype {dtype}")
+        self.n = tuple(int(v) for v in n)
+        self.dtype = dtype
+        self.layout = native().layout(list(self.n), torch.tensor([], dtype=dtype).element_size())
+        self.flat = torch.zeros(self.layout["elems"], dtype=dtype, device=device)
+
+    @property
+    def device(self):
+        return self.flat.device
+
+    @property
+    def dt(self) -> str:
+        return _DT[self.dtype]
+
+    def ghosted(self) -> torch.Tensor:
+        """View (n0+2, n1+2, n2+2) including the ghost shell."""
+        L = self.layout
+        off = L["origin"] - L["sx"] - L["sy"] - 1
+        shape = tuple(v + 2 for v in self.n)
+        return self.flat.as_strided(shape, (L["sx"], L["sy"], 1), off)
+
+    def owned(self) -> torch.Tensor:
+        L = self.layout
+        return self.flat.as_strided(self.n, (L["sx"], L["sy"], 1), L["origin"])
+
+    def data_ptr(self) -> int:
+        return self.flat.data_ptr()
+
+
+def _stream_ptr(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def ftcs_step(src: PaddedField, dst: PaddedField, D: Sequence[float],
+              box: Optional[Sequence[int]] = None, kernel: str = "auto",
+              state: Optional[torch.Tensor] = None, slot: int = 0) -> None:
+    """dst[box] = FTCS(src) on the owned box (default: all owned points).
+
+    ``state``: optional uint8/int64 tensor of ``DEVICE_STATE_BYTES`` that
+    receives the fused max-residual (IEEE bits of a double in its first
+    8 bytes for slot 0) and whose ``done`` word turns the kernel into a no-op.
+    """
+    if src.layout != dst.layout or src.dtype != dst.dtype or src.device != dst.device:
+        raise ValueError("src and dst must share layout, dtype and device")
+    n = src.n
+    b = list(box) if box is not None else [0, n[0], 0, n[1], 0, n[2]]
+    for a in range(3):
+        if not (0 <= b[2 * a] <= b[2 * a + 1] <= n[a]):
+            raise ValueError(f"box {b} outside owned extents {n}")
+    sptr = 0
+    if state is not None:
+        if state.device != src.device or state.numel() * state.element_size() < native().DEVICE_STATE_BYTES:
+            raise ValueError("state tensor too small or on the wrong device")
+        sptr = state.data_ptr()
+    ext = native()
+    if src.device.type == "cuda":
+        ext.hip.stencil(src.dt, src.data_ptr(), dst.data_ptr(), list(n), b, list(D), sptr, slot,
+                        kernel, _stream_ptr(src.flat))
+    else:
+        ext.cpu.stencil(src.dt, src.data_ptr(), dst.data_ptr(), list(n), b, list(D), sptr, slot)
+
+
+def init_field(f: PaddedField, gstart: Sequence[int], N: Sequence[int], h: Sequence[float]) -> None:
+    """Analytic IC/BC into the padded field (reference heat3D.cu:408-453)."""
+    ext = native()
+    if f.device.type == "cuda":
+        ext.hip.init_field(f.dt, f.data_ptr(), list(f.n), list(gstart), list(N), list(h), _stream_ptr(f.flat))
+    else:
+        ext.cpu.init_field(f.dt, f.data_ptr(), list(f.n), list(gstart), list(N), list(h))
+
+
+def pack_box(f: PaddedField, box: Sequence[int], out: torch.Tensor) -> None:
+    """Copy a local box (ghost indices allowed, -1..n) into a contiguous buffer (GPU)."""
+    native().hip.pack_box(f.dt, f.data_ptr(), list(f.n), list(box), out.data_ptr(), _stream_ptr(f.flat))
+
+
+def unpack_box(f: PaddedField, box: Sequence[int], buf: torch.Tensor) -> None:
+    native().hip.unpack_box(f.dt, f.data_ptr(), list(f.n), list(box), buf.data_ptr(), _stream_ptr(f.flat))
+
+
+def ftcs_reference(T: torch.Tensor, D: Sequence[float]) -> Tuple[torch.Tensor, float]:
+    """Plain-PyTorch FTCS on a ghosted block; returns (new interior, max |dT|)."""
+    c = T[1:-1, 1:-1, 1:-1]
+    c2 = 2.0 * c
+    ax = (T[2:, 1:-1, 1:-1] - c2) + T[:-2, 1:-1, 1:-1]
+    ay = (T[1:-1, 2:, 1:-1] - c2) + T[1:-1, :-2, 1:-1]
+    az = (T[1:-1, 1:-1, 2:] - c2) + T[1:-1, 1:-1, :-2]
+    new = ((c + D[0] * ax) + D[1] * ay) + D[2] * az
+    res = (new.double() - c.double()).abs().max().item() if new.numel() else 0.0
+    return new, res
+
+
+def residual_from_state(state: torch.Tensor, slot: int = 0) -> float:
+    """Decode the fused residual (double bits) written by ftcs_step."""
+    raw = state.detach().cpu().contiguous().view(torch.uint8)[8 * slot: 8 * slot + 8]
+    return float(raw.view(torch.float64).item())
+
+
+def new_state(device, eps: float = 0.0) -> torch.Tensor:
+    """Zeroed DeviceState buffer with the residual slots at their initial value."""
+    ext = native()
+    st = torch.zeros(ext.DEVICE_STATE_BYTES // 8, dtype=torch.int64)
+    init = ext.RESIDUAL_INIT_BITS
+    st[0] = init if init < 2 ** 63 else init - 2 ** 64
+    st[1] = st[0]
+    return st.to(device)

@@ -1,0 +1,11 @@
+"""Topology, decomposition and communicator bootstrap.
+
+Per-iteration traffic is native (RCCL over xGMI / sockets, csrc/comm);
+torch.distributed only bootstraps it (distributed.py).  torch_reference.py is
+an independent pure-PyTorch distributed oracle used by the tests.
+"""
+from .topology import (best_dims_for, decompose, dims_create, field_bytes_per_rank,  # noqa: F401
+                       halo_bytes_per_iteration, reference_legal)
+
+__all__ = ["dims_create", "decompose", "reference_legal", "halo_bytes_per_iteration",
+           "field_bytes_per_rank", "best_dims_for"]

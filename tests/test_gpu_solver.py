@@ -1,0 +1,110 @@
+"""End-to-end native solver on the MI355X: goldens, decomposition invariance,
+graph vs eager, overlap vs no overlap, RCCL (1 rank), checkpoint/restart."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(h3d, n, eps, iters=10 ** 6, **kw):
+    s = h3d.HeatSolver((n, n, n), iters, eps, backend=kw.pop("backend", "hip"), **kw)
+    r = s.run()
+    return s, r
+
+
+def test_native_extension_is_in_tree(h3d, gpu):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    assert os.path.abspath(h3d.native().__file__).startswith(root)
+
+
+@pytest.mark.parametrize("n,eps", [(27, 1e-3), (27, 1e-5), (33, 1e-5), (64, 1e-3), (64, 1e-4), (65, 1e-5),
+                                   (129, 1e-3)])
+def test_goldens_gpu(h3d, gpu, n, eps):
+    it, err, norm = h3d.utils.golden(n, eps)
+    s, r = _solve(h3d, n, eps)
+    assert s.backend == "hip"
+    assert r["converged"] and r["conv_iter"] == it, r
+    assert abs(r["error_percent"] - err) < 6e-5, r
+    assert abs(r["norm"] - norm) < 1e-6
+
+
+@pytest.mark.slow
+def test_golden_129_1e5_gpu(h3d, gpu):
+    it, err, _ = h3d.utils.golden(129, 1e-5)
+    s, r = _solve(h3d, 129, 1e-5)
+    assert r["conv_iter"] == it and abs(r["error_percent"] - err) < 6e-5, r
+
+
+def test_gpu_equals_cpu_bitwise(h3d, gpu):
+    sg, rg = _solve(h3d, 41, 1e-4)
+    sc, rc = _solve(h3d, 41, 1e-4, backend="cpu")
+    assert rg["conv_iter"] == rc["conv_iter"]
+    assert np.array_equal(sg.gather(), sc.gather())
+
+
+@pytest.mark.parametrize("vr,decomp", [(2, None), (4, None), (8, None), (8, (8, 1, 1)), (6, (1, 3, 2)),
+                                       (8, (2, 2, 2))])
+def test_virtual_ranks_bitwise(h3d, gpu, vr, decomp):
+    s1, r1 = _solve(h3d, 37, 1e-4)
+    sp, rp = _solve(h3d, 37, 1e-4, virtual_ranks=vr, decomp=decomp)
+    assert rp["conv_iter"] == r1["conv_iter"]
+    assert np.array_equal(s1.gather(), sp.gather())
+
+
+@pytest.mark.parametrize("graph,overlap", [(False, False), (False, True), (True, False), (True, True)])
+def test_schedules_bitwise(h3d, gpu, graph, overlap):
+    base, rb = _solve(h3d, 45, 1e-4, virtual_ranks=4, graph=False, overlap=False, check_every=1)
+    s, r = _solve(h3d, 45, 1e-4, virtual_ranks=4, graph=graph, overlap=overlap, check_every=7,
+                  graph_chunk=6)
+    assert r["conv_iter"] == rb["conv_iter"]
+    assert np.array_equal(s.gather(), base.gather())
+
+
+@pytest.mark.parametrize("kernel", ["naive", "column:2:4", "column:2:8", "column:1:8"])
+def test_kernel_variants_solver(h3d, gpu, kernel):
+    s, r = _solve(h3d, 64, 1e-3, kernel=kernel)
+    assert r["conv_iter"] == 1915
+
+
+def test_rccl_single_rank(h3d, gpu):
+    """RcclComm with nranks = 1 (the installed RCCL refuses two ranks per GPU)."""
+    ext = h3d.native()
+    uid = ext.rccl_unique_id()
+    assert len(uid) == 128
+    s = ext.Solver(["33", "33", "33", "10000", "1e-5", "--backend", "hip"], rank=0, size=1, comm="rccl",
+                   unique_id=uid, device=0)
+    s.initialize()
+    r = s.run()
+    assert r["converged"] and r["conv_iter"] == 3590
+    assert s.comm_name == "rccl"
+
+
+def test_fp32_solver(h3d, gpu):
+    sg, rg = _solve(h3d, 33, 1e-4, dtype="fp32")
+    sc, rc = _solve(h3d, 33, 1e-4, dtype="fp32", backend="cpu")
+    assert rg["conv_iter"] == rc["conv_iter"]
+    assert np.array_equal(sg.gather(), sc.gather())
+    it64 = _solve(h3d, 33, 1e-4)[1]["conv_iter"]
+    assert abs(rg["conv_iter"] - it64) <= 5
+
+
+def test_checkpoint_restart_gpu(h3d, gpu, tmp_path):
+    full, rf = _solve(h3d, 31, 1e-4)
+    a = h3d.HeatSolver((31, 31, 31), 500, 1e-4, backend="hip")
+    a.run()
+    a.save_checkpoint(str(tmp_path / "ck"))
+    b = h3d.HeatSolver((31, 31, 31), 10 ** 6, 1e-4, backend="hip", virtual_ranks=4,
+                       extra_args=["--restart", str(tmp_path / "ck")])
+    rb = b.run()
+    assert rb["conv_iter"] == rf["conv_iter"]
+    assert np.array_equal(b.gather(), full.gather())
+
+
+def test_nan_fault_detected(h3d, gpu):
+    s = h3d.HeatSolver((21, 21, 21), 1000, 1e-9, backend="hip")
+    s.initialize()
+    s.native.inject(0, 5, 5, 5, float("nan"))
+    r = s.run()
+    assert r["fault"] and not r["converged"]
