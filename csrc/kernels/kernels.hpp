@@ -70,6 +70,8 @@ int64_t error_scratch_elems();
 // Fault injection (tests): write `value` at local owned point (i,j,k).
 void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k, double value,
           void* stream);
+// HBM calibration: kind 0 = 16 B/lane copy src->dst, 1 = 16 B/lane read of src.
+void bandwidth_probe(int kind, const void* src, void* dst, int64_t bytes, int blocks, void* stream);
 }  // namespace hip
 
 namespace cpu {

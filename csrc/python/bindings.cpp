@@ -8,6 +8,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <cstdlib>
 #include <cstring>
 
 #include "../comm/comm.hpp"
@@ -126,12 +131,31 @@ StencilParams sparams(int64_t in_ptr, int64_t out_ptr, const std::array<int64_t,
   return p;
 }
 
+// HEAT3D_SEGV_TRACE=1: print the native backtrace on SIGSEGV/SIGBUS/SIGFPE
+// (no debugger on the GPU boxes), then re-raise with the default action.
+void segv_trace(int sig) {
+  void* frames[64];
+  int n = backtrace(frames, 64);
+  const char msg[] = "\nheat3d: fatal signal, native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+void install_segv_trace() {
+  const char* e = std::getenv("HEAT3D_SEGV_TRACE");
+  if (!e || !*e || e[0] == '0') return;
+  for (int s : {SIGSEGV, SIGBUS, SIGFPE, SIGILL}) signal(s, segv_trace);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_heat3d, m) {
+  install_segv_trace();
   m.doc() = "heat3d-mi355x native runtime (HIP/gfx950 kernels, RCCL/socket comm, solver)";
-  py::register_exception<UsageError>(m, "UsageError");
-  py::register_exception<Error>(m, "NativeError");
+  auto native_error = py::register_exception<Error>(m, "NativeError", PyExc_RuntimeError);
+  py::register_exception<UsageError>(m, "UsageError", native_error.ptr());
 
   m.def("device_count", &hip_device_count);
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
@@ -231,6 +255,10 @@ PYBIND11_MODULE(_heat3d, m) {
     DType t = dt_of(dt);
     hip::unpack_box(t, reinterpret_cast<void*>(f), to_layout(n, (int64_t)dtype_size(t)), to_box(box),
                     reinterpret_cast<void*>(buf), reinterpret_cast<void*>(stream));
+  });
+  hk.def("bandwidth_probe", [](int kind, int64_t src, int64_t dst, int64_t bytes, int blocks, int64_t stream) {
+    hip::bandwidth_probe(kind, reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), bytes, blocks,
+                         reinterpret_cast<void*>(stream));
   });
   hk.def("check_convergence", [](int64_t state_ptr, int slot, int64_t stream) {
     hip::check_convergence(reinterpret_cast<DeviceState*>(state_ptr), slot, reinterpret_cast<void*>(stream));

@@ -80,7 +80,7 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   dstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
   hstate_ = static_cast<DeviceState*>(be_->alloc_host(2 * sizeof(DeviceState)));
   std::memset(hstate_, 0, 2 * sizeof(DeviceState));
-  for (auto& e : ev_) e = be_->event_create();
+  for (int i = 0; i < EV_COUNT; ++i) cur_ev_[i] = ev_[i] = be_->event_create();
 }
 
 Solver::~Solver() {
@@ -91,6 +91,7 @@ Solver::~Solver() {
   if (graph_) be_->destroy_graph(graph_);
   for (auto& e : ev_)
     if (e) be_->event_destroy(e);
+  for (auto& e : cap_pool_) be_->event_destroy(e);
   for (auto& l : local_) {
     for (auto* f : l.field) be_->release(f);
     for (auto& io : l.faces) {
@@ -164,12 +165,20 @@ InitParams Solver::init_params(const Local& l) const {
 }
 
 void Solver::ev_record(int id, StreamId s) {
-  be_->record(ev_[id], s);
+  if (capturing_) {
+    // inside a stream capture every record gets a fresh event (the HIP
+    // runtime does not tolerate re-recording one event within a capture)
+    HEAT3D_CHECK(cap_next_ < cap_pool_.size(), "capture event pool exhausted");
+    cur_ev_[id] = cap_pool_[cap_next_++];
+  } else {
+    cur_ev_[id] = ev_[id];
+  }
+  be_->record(cur_ev_[id], s);
   ev_valid_[id] = true;
 }
 
 void Solver::ev_wait(StreamId s, int id) {
-  if (ev_valid_[id]) be_->wait(s, ev_[id]);
+  if (ev_valid_[id]) be_->wait(s, cur_ev_[id]);
 }
 
 void Solver::initialize() {
@@ -250,7 +259,25 @@ void Solver::enqueue_halo(int p) {
   be_->range_pop();
 }
 
+static bool trace_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT3D_TRACE");
+    return e && *e && e[0] != '0';
+  }();
+  return on;
+}
+#define H3D_TRACE(msg)                                                   \
+  do {                                                                   \
+    if (trace_on()) {                                                    \
+      std::ostringstream _os;                                            \
+      _os << "[heat3d trace] " << msg << "\n";                           \
+      std::fputs(_os.str().c_str(), stderr);                             \
+      std::fflush(stderr);                                               \
+    }                                                                    \
+  } while (0)
+
 void Solver::enqueue_iteration(int p) {
+  H3D_TRACE("iteration issued=" << issued_ << " parity=" << p << (capturing_ ? " (capturing)" : ""));
   auto params = [&](Local& l, const Box& b) {
     StencilParams sp;
     sp.in = l.field[p];
@@ -296,24 +323,32 @@ void Solver::enqueue_iteration(int p) {
 }
 
 void Solver::build_graph() {
+  H3D_TRACE("build_graph at issued=" << issued_);
   const int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
   graph_parity_ = (int)(issued_ & 1);
   bool saved[EV_COUNT];
   std::memcpy(saved, ev_valid_, sizeof(saved));
+  Event saved_cur[EV_COUNT];
+  std::memcpy(saved_cur, cur_ev_, sizeof(saved_cur));
+  const std::size_t need = 8 * (std::size_t)G + 8;
+  while (cap_pool_.size() < need) cap_pool_.push_back(be_->event_create());
+  cap_next_ = 0;
   try {
     be_->begin_capture();
     capturing_ = true;
     for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
     ev_record(EV_FORK, kCompute);
-    be_->wait(kComm, ev_[EV_FORK]);
-    be_->wait(kReduce, ev_[EV_FORK]);
+    ev_wait(kComm, EV_FORK);
+    ev_wait(kReduce, EV_FORK);
     for (int i = 0; i < G; ++i) enqueue_iteration((graph_parity_ + i) & 1);
     ev_record(EV_JCOMM, kComm);
     ev_record(EV_JRED, kReduce);
-    be_->wait(kCompute, ev_[EV_JCOMM]);
-    be_->wait(kCompute, ev_[EV_JRED]);
+    ev_wait(kCompute, EV_JCOMM);
+    ev_wait(kCompute, EV_JRED);
+    H3D_TRACE("end_capture");
     graph_ = be_->end_capture();
     capturing_ = false;
+    H3D_TRACE("graph instantiated");
     graph_iters_ = G;
   } catch (const std::exception& e) {
     if (capturing_) {
@@ -329,24 +364,34 @@ void Solver::build_graph() {
       std::fprintf(stderr, "heat3d: hipGraph capture failed (%s); running eagerly\n", e.what());
   }
   std::memcpy(ev_valid_, saved, sizeof(saved));
+  std::memcpy(cur_ev_, saved_cur, sizeof(saved_cur));
 }
 
 void Solver::run_chunk(int64_t n) {
+  // The overlapped schedule forks the comm stream; hipStreamEndCapture of that
+  // three-stream pattern crashes on ROCm 7.0/7.2 (see docs/ARCHITECTURE.md), so
+  // graphs are used for the single-stream schedules (the launch-bound small
+  // and single-GPU cases) unless HEAT3D_GRAPH_MULTISTREAM=1.
+  static const bool ms_ok = [] {
+    const char* e = std::getenv("HEAT3D_GRAPH_MULTISTREAM");
+    return e && e[0] == '1';
+  }();
   const bool graphs = cfg_.use_graph && be_->supports_graphs() && comm_->capturable() &&
-                      !graph_failed_ && !phase_timing_;
+                      !graph_failed_ && !phase_timing_ && (!overlap_ || ms_ok);
   while (n > 0) {
     const int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
     if (graphs && n >= G && (graph_ == nullptr || (int)(issued_ & 1) == graph_parity_)) {
       if (!graph_) build_graph();
       if (graph_ && (int)(issued_ & 1) == graph_parity_) {
+        H3D_TRACE("launch_graph issued=" << issued_);
         be_->launch_graph(graph_);
         issued_ += graph_iters_;
         n -= graph_iters_;
         // the graph joined every stream into compute: re-fork for eager work
         for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
         ev_record(EV_FORK, kCompute);
-        be_->wait(kComm, ev_[EV_FORK]);
-        be_->wait(kReduce, ev_[EV_FORK]);
+        ev_wait(kComm, EV_FORK);
+        ev_wait(kReduce, EV_FORK);
         continue;
       }
     }
@@ -356,8 +401,8 @@ void Solver::run_chunk(int64_t n) {
     enqueue_iteration((int)(issued_ & 1));
     if (phase_timing_) {
       ev_record(EV_T1, kReduce);
-      be_->event_sync(ev_[EV_T1]);
-      double ms = be_->elapsed_ms(ev_[EV_T0], ev_[EV_T1]);
+      be_->event_sync(cur_ev_[EV_T1]);
+      double ms = be_->elapsed_ms(cur_ev_[EV_T0], cur_ev_[EV_T1]);
       if (phase_acc_.empty()) phase_acc_.push_back({"iteration_ms", 0.0});
       phase_acc_[0].second += ms;
     }
@@ -414,7 +459,7 @@ RunResult Solver::run() {
     if (have_prev) {
       const int q = pslot ^ 1;
       const double tw = now_s();
-      while (!be_->query(ev_[EV_POLL + q])) {
+      while (!be_->query(cur_ev_[EV_POLL + q])) {
         comm_->check_async_error();
         if (now_s() - tw > watchdog) {
           comm_->abort();

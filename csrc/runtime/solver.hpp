@@ -159,6 +159,9 @@ class Solver {
   enum { EV_INT = 0, EV_BND = 2, EV_CHK = 4, EV_FORK = 6, EV_JCOMM = 7, EV_JRED = 8, EV_POLL = 9,
          EV_T0 = 11, EV_T1 = 12, EV_COUNT = 16 };
   Event ev_[EV_COUNT] = {};
+  Event cur_ev_[EV_COUNT] = {};     // event currently standing for each id
+  std::vector<Event> cap_pool_;     // fresh events for records inside a capture
+  std::size_t cap_next_ = 0;
   bool ev_valid_[EV_COUNT] = {};
   bool capturing_ = false;
 

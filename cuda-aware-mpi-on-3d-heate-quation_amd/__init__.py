@@ -26,6 +26,7 @@ __version__ = "0.1.0"
 from . import _native  # noqa: F401  (imports torch first: one HIP runtime)
 from ._native import available as native_available  # noqa: F401
 from ._native import native  # noqa: F401
+from . import models, ops, parallel, utils  # noqa: F401,E402
 from .models.heat3d import HeatEquation3D, HeatSolver  # noqa: F401
 
 __all__ = ["HeatEquation3D", "HeatSolver", "native", "native_available", "__version__"]

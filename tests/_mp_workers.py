@@ -1,0 +1,67 @@
+"""Worker functions for multi-process CPU tests (gloo, world_size > 1).
+
+Each worker initialises torch.distributed (gloo, 127.0.0.1), runs a solver and
+saves its results to ``outdir`` so the parent test can compare them.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _init(rank, world, port):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    return dist
+
+
+def native_socket_worker(rank, world, port, outdir, n, eps, decomp, dtype):
+    """Native engine, CPU backend, SocketComm bootstrapped through gloo."""
+    dist = _init(rank, world, port)
+    import heat3d_amd
+
+    s = heat3d_amd.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", decomp=decomp, dtype=dtype,
+                              threads=2)
+    assert s.native.comm_name == "socket"
+    r = s.run()
+    g = s.gather()
+    ck = os.path.join(outdir, "ckpt")
+    s.save_checkpoint(ck)
+    s.write_tecplot(os.path.join(outdir, "out.dat"), "owned")
+    if rank == 0:
+        np.save(os.path.join(outdir, "field.npy"), g)
+        with open(os.path.join(outdir, "result.txt"), "w") as f:
+            f.write(f"{r['conv_iter']} {r['error_percent']!r} {r['norm']!r} {list(s.dims)}\n")
+    else:
+        assert g is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def torch_reference_worker(rank, world, port, outdir, n, eps, decomp):
+    """Pure-torch distributed oracle (gloo point-to-point halos)."""
+    dist = _init(rank, world, port)
+    import torch
+
+    from heat3d_amd.parallel.torch_reference import TorchReferenceSolver
+
+    s = TorchReferenceSolver((n, n, n), eps, 10 ** 6, dims=decomp)
+    r = s.run()
+    e, c = s.error_sum()
+    t = torch.tensor([e, float(c)], dtype=torch.float64)
+    dist.all_reduce(t)
+    np.save(os.path.join(outdir, f"interior_{rank}.npy"), s.interior().numpy())
+    with open(os.path.join(outdir, f"sub_{rank}.txt"), "w") as f:
+        f.write(" ".join(str(v) for v in s.sub.gstart + s.sub.n) + "\n")
+    if rank == 0:
+        with open(os.path.join(outdir, "result.txt"), "w") as f:
+            f.write(f"{r['conv_iter']} {100.0 * t[0].item() / t[1].item()!r}\n")
+    dist.barrier()
+    dist.destroy_process_group()

@@ -1,0 +1,112 @@
+"""CLI contract (reference heat3D.cu:270-315, 1078-1106)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, free_port, run_cli
+
+REF_OUT = "/root/reference/HeatEquation3D/output/out.dat"
+
+
+def test_config_parse(ext):
+    c = ext.config_parse(["27", "28", "29", "100", "1e-5", "--dtype", "fp32", "--decomp", "2x1x1"])
+    assert tuple(c["n"]) == (27, 28, 29) and c["iter_max"] == 100 and c["eps"] == 1e-5
+    assert c["dtype"] == "fp32" and tuple(c["decomp"]) == (2, 1, 1)
+    for bad in (["27", "27", "27", "100"], ["a", "1", "1", "1", "1"], ["27"] * 3 + ["1", "x"],
+                ["2", "27", "27", "1", "1"], ["27"] * 3 + ["1", "1", "--bogus"], ["27"] * 3 + ["1", "1", "--decomp", "2x2"]):
+        with pytest.raises(ext.UsageError):
+            ext.config_parse(bad)
+
+
+def test_physics_constants(ext):
+    p = ext.physics(27, 27, 27)
+    assert p["h"][0] == 1.0 / 26.0
+    # D = dt / h^2 = CFL / 6 = 1/15 on a cube
+    assert all(abs(d - 1 / 15) < 1e-15 for d in p["D"])
+    q = ext.physics(11, 21, 41)
+    hmin = min(q["h"])
+    assert abs(q["dt"] - 0.4 / 6 * hmin ** 2) < 1e-18
+
+
+def test_banner_exact_bytes(heat3d_bin, tmp_path):
+    r = run_cli(["27", "27", "27", "100", "1e-05", "--backend", "cpu", "--output", "none"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.split("\n")
+    assert lines[0] == "Runnung HeatEquation3D with the following arguments: "
+    assert lines[1] == f"executable:               {heat3d_bin}"
+    assert lines[2:7] == ["number of cells in x:     27", "number of cells in y:     27",
+                          "number of cells in z:     27", "max number of iterations: 100",
+                          "convergence threshold:    1e-05"]
+    assert lines[7] == ""
+    assert lines[8].startswith("Computational time (parallel): ")
+    assert len(lines[8].split(": ")[1].split(".")[1]) == 6
+    assert lines[9] == ""
+    assert lines[10] == "Simulation did not converge within 100 iterations."
+    assert lines[11] == "L2-norm error: 26.0129 %"
+
+
+def test_converged_report_and_output(heat3d_bin, tmp_path):
+    r = run_cli(["27", "27", "27", "100000", "1e-5", "--backend", "cpu", "--json-out", "run.json"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "Simulation has converged in 2513 iterations with a convergence threshold of 1.000000e-05" in r.stdout
+    assert "L2-norm error: 0.0192 %" in r.stdout
+    out = (tmp_path / "output" / "out.dat").read_text().split("\n")
+    ref = open(REF_OUT).read().split("\n")
+    assert out[:3] == ref[:3]  # header byte-compatible with the shipped artifact
+    assert len(out) == len(ref)
+    # coordinate columns identical to the reference artifact (T differs: its run was broken)
+    for a, b in zip(out[3:200], ref[3:200]):
+        assert a[:45] == b[:45]
+    j = json.loads((tmp_path / "run.json").read_text())
+    assert j["conv_iter"] == 2513 and j["converged"] and j["backend"] == "cpu"
+
+
+def test_usage_error_exit_code(heat3d_bin, tmp_path):
+    r = run_cli(["27", "27"], tmp_path)
+    assert r.returncode != 0
+    assert "bin/HeatEquation3D NUM_CELLS_X NUM_CELLS_Y NUM_CELLS_Z ITER_MAX EPS" in r.stdout
+
+
+def test_virtual_ranks_cli_ref_layout(heat3d_bin, tmp_path):
+    # 27^3 on 8 virtual ranks: reference-legal -> 8 zones of 14^3 with a rank column
+    r = run_cli(["27", "27", "27", "100000", "1e-4", "--backend", "cpu", "--virtual-ranks", "8"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "converged in 1725 iterations" in r.stdout
+    lines = (tmp_path / "output" / "out.dat").read_text().split("\n")
+    assert lines[1] == 'VARIABLES = "X", "Y", "Z", "T", "rank"'
+    assert lines[2] == 'ZONE T = "0", I=14, J=14, K=14, F=POINT'
+    assert lines[3 + 14 ** 3] == 'ZONE T = "1", I=14, J=14, K=14, F=POINT'
+    assert lines[4].endswith("    0") and len(lines[4]) == 65
+
+
+def test_compat_zone_titles(heat3d_bin, tmp_path):
+    r = run_cli(["27", "27", "27", "10", "1e-4", "--backend", "cpu", "--virtual-ranks", "2", "--compat"], tmp_path)
+    assert r.returncode == 0
+    txt = (tmp_path / "output" / "out.dat").read_text()
+    assert txt.count('ZONE T = "0"') == 2  # reference bug A14 reproduced under --compat
+
+
+def test_cli_multiprocess_socket(heat3d_bin, tmp_path):
+    """Two CLI processes (torchrun-style env) over the socket transport."""
+    import subprocess
+
+    port = free_port()
+    env = {"WORLD_SIZE": "2", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+           "HEAT3D_BOOTSTRAP_PORT": str(port)}
+    procs = []
+    for r in range(2):
+        e = dict(os.environ)
+        e.update(env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r)})
+        procs.append(subprocess.Popen([heat3d_bin, "27", "27", "27", "100000", "1e-4", "--backend", "cpu",
+                                       "--threads", "2"], cwd=tmp_path, env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "converged in 1725 iterations" in outs[0][0]
+    assert "comm=socket ranks=2" in outs[0][0]
+    assert outs[1][0] == ""  # only rank 0 reports
+    zones = (tmp_path / "output" / "out.dat").read_text().count("ZONE")
+    assert zones == 2

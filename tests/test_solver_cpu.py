@@ -1,0 +1,136 @@
+"""Native engine on the CPU backend: goldens, decomposition
+invariance (bitwise), schedules, checkpoint/restart, fault detection, ops."""
+import numpy as np
+import pytest
+import torch
+
+
+def _solve(h3d, n, eps, iters=10 ** 6, **kw):
+    s = h3d.HeatSolver((n, n, n) if isinstance(n, int) else n, iters, eps, backend="cpu", **kw)
+    return s, s.run()
+
+
+@pytest.mark.parametrize("n,eps", [(27, 1e-3), (27, 1e-4), (27, 1e-5), (33, 1e-5), (64, 1e-3)])
+def test_goldens_cpu(h3d, n, eps):
+    it, err, norm = h3d.utils.golden(n, eps)
+    s, r = _solve(h3d, n, eps)
+    assert r["converged"] and r["conv_iter"] == it
+    assert abs(r["error_percent"] - err) < 6e-5
+    assert abs(r["norm"] - norm) < 1e-6
+
+
+def test_itermax_not_converged(h3d):
+    s, r = _solve(h3d, 27, 1e-5, iters=100)
+    assert not r["converged"] and r["iterations"] == 100
+    assert abs(r["error_percent"] - h3d.utils.goldens.ITERMAX_100_27) < 6e-5
+
+
+@pytest.mark.parametrize("vr,decomp", [(2, None), (3, None), (4, (1, 2, 2)), (8, None), (8, (8, 1, 1)),
+                                       (12, None)])
+def test_virtual_ranks_bitwise(h3d, vr, decomp):
+    s1, r1 = _solve(h3d, 29, 1e-4)
+    s2, r2 = _solve(h3d, 29, 1e-4, virtual_ranks=vr, decomp=decomp)
+    assert r1["conv_iter"] == r2["conv_iter"]
+    assert np.array_equal(s1.gather(), s2.gather())
+    assert r1["error_percent"] == pytest.approx(r2["error_percent"], rel=1e-12)
+
+
+def test_anisotropic_grid_invariance(h3d):
+    s1, r1 = _solve(h3d, (31, 17, 23), 1e-4)
+    s2, r2 = _solve(h3d, (31, 17, 23), 1e-4, virtual_ranks=6, decomp=(3, 2, 1))
+    assert r1["conv_iter"] == r2["conv_iter"]
+    assert np.array_equal(s1.gather(), s2.gather())
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_overlap_schedule_same_result(h3d, overlap):
+    s1, r1 = _solve(h3d, 25, 1e-4, virtual_ranks=4, overlap=True, check_every=1)
+    s2, r2 = _solve(h3d, 25, 1e-4, virtual_ranks=4, overlap=overlap, check_every=13)
+    assert r1["conv_iter"] == r2["conv_iter"]
+    assert np.array_equal(s1.gather(), s2.gather())
+
+
+def test_fp32_close_to_fp64(h3d):
+    s64, r64 = _solve(h3d, 27, 1e-4)
+    s32, r32 = _solve(h3d, 27, 1e-4, dtype="fp32")
+    assert abs(r32["conv_iter"] - r64["conv_iter"]) <= 5
+    assert np.max(np.abs(s32.gather() - s64.gather())) < 1e-4
+
+
+def test_step_and_state(h3d):
+    s = h3d.HeatSolver((21, 21, 21), 10 ** 6, 0.0, backend="cpu")
+    s.initialize()
+    s.step(37)
+    s.synchronize()
+    st = s.state()
+    assert st["iter"] == 37 and st["done"] == 0 and st["conv_iter"] == -1
+
+
+def test_gather_matches_model_initial_field(h3d):
+    s = h3d.HeatSolver((13, 11, 9), 10, 1e-3, backend="cpu", virtual_ranks=4)
+    s.initialize()
+    g = s.gather()
+    assert np.array_equal(g, s.model.initial_field())
+
+
+@pytest.mark.parametrize("vr_restart", [1, 4])
+def test_checkpoint_restart(h3d, tmp_path, vr_restart):
+    full, rf = _solve(h3d, 23, 1e-4)
+    a = h3d.HeatSolver((23, 23, 23), 300, 1e-4, backend="cpu", virtual_ranks=2)
+    a.run()
+    a.save_checkpoint(str(tmp_path / "ck"))
+    b = h3d.HeatSolver((23, 23, 23), 10 ** 6, 1e-4, backend="cpu", virtual_ranks=vr_restart,
+                       extra_args=["--restart", str(tmp_path / "ck")])
+    rb = b.run()
+    assert rb["conv_iter"] == rf["conv_iter"]
+    assert np.array_equal(b.gather(), full.gather())
+
+
+def test_periodic_checkpoint_flag(h3d, tmp_path):
+    s = h3d.HeatSolver((17, 17, 17), 200, 1e-9, backend="cpu",
+                       extra_args=["--checkpoint-every", "64", "--checkpoint-dir", str(tmp_path / "p")])
+    s.run()
+    import json
+
+    meta = json.loads((tmp_path / "p" / "meta.json").read_text())
+    assert meta["iteration"] == 192 and meta["N"] == [17, 17, 17]
+
+
+def test_checkpoint_mismatch_rejected(h3d, tmp_path):
+    a = h3d.HeatSolver((15, 15, 15), 10, 1e-4, backend="cpu")
+    a.run()
+    a.save_checkpoint(str(tmp_path / "ck"))
+    with pytest.raises(Exception):
+        h3d.HeatSolver((17, 17, 17), 10, 1e-4, backend="cpu", extra_args=["--restart", str(tmp_path / "ck")]).run()
+
+
+def test_nan_fault_detected(h3d):
+    s = h3d.HeatSolver((21, 21, 21), 1000, 1e-9, backend="cpu", virtual_ranks=2)
+    s.initialize()
+    s.native.inject(1, 2, 3, 4, float("nan"))
+    r = s.run()
+    assert r["fault"] and not r["converged"] and r["conv_iter"] == 0
+
+
+def test_ops_cpu_bitwise(h3d):
+    ops = h3d.ops
+    for dt in (torch.float64, torch.float32):
+        f = ops.PaddedField((7, 9, 11), dtype=dt)
+        f.ghosted().copy_(torch.rand(9, 11, 13, dtype=torch.float64).to(dt))
+        g = ops.PaddedField((7, 9, 11), dtype=dt)
+        st = ops.new_state("cpu")
+        ops.ftcs_step(f, g, (0.05, 0.06, 0.07), state=st)
+        ref, res = ops.ftcs_reference(f.ghosted(), (0.05, 0.06, 0.07))
+        assert torch.equal(g.owned(), ref)
+        assert ops.residual_from_state(st) == res
+
+
+def test_model_matches_native_init(h3d):
+    m = h3d.HeatEquation3D((9, 10, 11))
+    ext = h3d.native()
+    f = h3d.ops.PaddedField((7, 8, 9))
+    h3d.ops.init_field(f, (1, 1, 1), m.n, m.h)
+    assert np.array_equal(f.ghosted().numpy(), m.initial_field())
+    for p in [(0, 3, 4), (3, 9, 4), (8, 0, 10), (4, 4, 4)]:
+        assert ext.boundary_value(*p, list(m.n), list(m.h)) == (m.boundary_value(*p) if
+                                                               0 in p or p[0] == 8 or p[1] == 9 or p[2] == 10 else 0.0)

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Kernel variant sweep for the gfx950 stencil (one process, interleaved rounds).
+
+Times ``ftcs_step`` ping-pong sweeps over an N^3 box for each kernel variant,
+alternating variants round by round (cdna_hip_programming.md §5.4 rule 24),
+and prints GLUPS / effective TB/s (16 B/point fp64, 8 B/point fp32).
+
+  python tools/tune.py --n 1024 --dtype fp64 --variants column:2:8 column:1:4 naive
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--dtype", default="fp64")
+    ap.add_argument("--variants", nargs="+", default=["column"])
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--json-out", default="")
+    a = ap.parse_args()
+
+    import torch
+
+    import heat3d_amd
+    from heat3d_amd import ops
+
+    dt = torch.float64 if a.dtype == "fp64" else torch.float32
+    n = (a.n - 2,) * 3
+    dev = torch.device("cuda", 0)
+    f0 = ops.PaddedField(n, dtype=dt, device=dev)
+    f1 = ops.PaddedField(n, dtype=dt, device=dev)
+    N = (a.n,) * 3
+    h = tuple(1.0 / (v - 1.0) for v in N)
+    ops.init_field(f0, (1, 1, 1), N, h)
+    ops.init_field(f1, (1, 1, 1), N, h)
+    f0.owned().copy_(torch.rand(n, dtype=dt, device=dev))
+    D = (1 / 15,) * 3
+    state = ops.new_state(dev)
+    pts = n[0] * n[1] * n[2]
+    esize = 8 if a.dtype == "fp64" else 4
+    res = {v: [] for v in a.variants}
+    for v in a.variants:  # warm / compile / validate
+        ops.ftcs_step(f0, f1, D, kernel=v, state=state)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(a.rounds):
+        for v in a.variants:
+            e0.record()
+            for i in range(a.iters):
+                src, dst = (f0, f1) if i % 2 == 0 else (f1, f0)
+                ops.ftcs_step(src, dst, D, kernel=v, state=state)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            res[v].append(pts / (ms * 1e-3) / 1e9)
+    # HBM calibration on the same buffers: 16 B/lane copy and read-only sweeps
+    ext = heat3d_amd.native()
+    nbytes = (f0.flat.numel() * esize) // 4096 * 4096
+    strm = torch.cuda.current_stream().cuda_stream
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    for blocks in (2048, 8192):
+        for kind, name in ((0, "copy"), (1, "read")):
+            ts = []
+            for _ in range(a.rounds):
+                e0.record()
+                for _ in range(a.iters):
+                    ext.hip.bandwidth_probe(kind, f0.data_ptr(), f1.data_ptr() if kind == 0 else sink.data_ptr(),
+                                            nbytes, blocks, strm)
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1) / a.iters)
+            moved = nbytes * (2 if kind == 0 else 1)
+            print(json.dumps({"probe": name, "blocks": blocks, "bytes": moved,
+                              "tbps": round(moved / (statistics.median(ts) * 1e-3) / 1e12, 3)}), flush=True)
+    out = []
+    for v in a.variants:
+        g = statistics.median(res[v])
+        out.append({"variant": v, "glups_median": round(g, 2), "glups_max": round(max(res[v]), 2),
+                    "tbps": round(g * 2 * esize / 1e3, 3), "n": a.n, "dtype": a.dtype})
+        print(json.dumps(out[-1]), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
