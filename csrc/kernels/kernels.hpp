@@ -16,10 +16,13 @@
 namespace heat3d {
 
 struct KernelSpec {
-  enum Kind { Naive = 0, Column = 1 } kind = Column;
+  enum Kind { Naive = 0, Column = 1, Tile = 2 } kind = Column;
+  int WZ = 0, WY = 0;  // tile kernel: waves per workgroup along z and y
   int V = 0;  // elements per lane along z (0 = default for dtype)
   int R = 0;  // rows per wave along y (0 = default)
   int L = 0;  // x-segment length per wave (0 = auto)
+  int O = -1; // tile order: 1 = z tiles fastest (default), 0 = y tiles fastest
+  int NT = 0; // non-temporal output stores
   static KernelSpec parse(const std::string& s);
   std::string str() const;
 };

@@ -32,16 +32,33 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     if (parts.size() > 1) k.V = std::atoi(parts[1].c_str());
     if (parts.size() > 2) k.R = std::atoi(parts[2].c_str());
     if (parts.size() > 3) k.L = std::atoi(parts[3].c_str());
+    if (parts.size() > 4) k.O = std::atoi(parts[4].c_str());
+    if (parts.size() > 5) k.NT = std::atoi(parts[5].c_str());
+  } else if (parts[0] == "tile") {
+    k.kind = Tile;
+    auto at = [&](std::size_t i) { return parts.size() > i ? std::atoi(parts[i].c_str()) : 0; };
+    k.V = at(1);
+    k.R = at(2);
+    k.WZ = at(3);
+    k.WY = at(4);
+    k.L = at(5);
+    k.NT = at(6);
   } else {
-    throw UsageError("unknown kernel '" + s + "' (auto | naive | column[:V[:R[:L]]])");
+    throw UsageError("unknown kernel '" + s +
+                     "' (auto | naive | column[:V[:R[:L[:O[:NT]]]]] | tile[:V[:R[:WZ[:WY[:L[:NT]]]]]])");
   }
   return k;
 }
 
 std::string KernelSpec::str() const {
   if (kind == Naive) return "naive";
+  if (kind == Tile) {
+    std::ostringstream os;
+    os << "tile:" << V << ":" << R << ":" << WZ << ":" << WY << ":" << L << ":" << NT;
+    return os.str();
+  }
   std::ostringstream os;
-  os << "column:" << V << ":" << R << ":" << L;
+  os << "column:" << V << ":" << R << ":" << L << ":" << O << ":" << NT;
   return os.str();
 }
 
