@@ -60,11 +60,17 @@ class RcclComm final : public Comm {
     std::memcpy(&id, uid.data(), sizeof(id));
     if (hipSetDevice(device) != hipSuccess) HEAT3D_THROW("hipSetDevice(" << device << ") failed");
     NCCL_CHECK(ncclCommInitRank(&halo_, size_, id, rank_));
-    NCCL_CHECK(ncclCommSplit(halo_, 0, rank_, &red_, nullptr));
+    // A second communicator for the per-iteration scalar all-reduce; if the
+    // runtime RCCL cannot split, reductions share the halo communicator
+    // (still correct: every rank issues both streams' ops in one order).
+    if (ncclCommSplit(halo_, 0, rank_, &red_, nullptr) != ncclSuccess || red_ == nullptr) {
+      red_ = halo_;
+      shared_ = true;
+    }
   }
   ~RcclComm() override {
     if (bar_) (void)hipFree(bar_);
-    if (red_) ncclCommDestroy(red_);
+    if (red_ && !shared_) ncclCommDestroy(red_);
     if (halo_) ncclCommDestroy(halo_);
   }
   const char* name() const override { return "rccl"; }
@@ -114,7 +120,7 @@ class RcclComm final : public Comm {
     }
   }
   void abort() override {
-    if (red_) ncclCommAbort(red_);
+    if (red_ && !shared_) ncclCommAbort(red_);
     if (halo_) ncclCommAbort(halo_);
     red_ = halo_ = nullptr;
   }
@@ -122,6 +128,7 @@ class RcclComm final : public Comm {
  private:
   int rank_, size_;
   ncclComm_t halo_ = nullptr, red_ = nullptr;
+  bool shared_ = false;
   void* bar_ = nullptr;
 };
 

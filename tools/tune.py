@@ -66,18 +66,19 @@ def main():
     nbytes = (f0.flat.numel() * esize) // 4096 * 4096
     strm = torch.cuda.current_stream().cuda_stream
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
-    for blocks in (2048, 8192):
-        for kind, name in ((0, "copy"), (1, "read")):
+    probes = ((0, "copy"), (1, "read"), (2, "copy_x4"), (3, "copy_x4_nt"), (4, "copy_chunk"))
+    for blocks in (1024, 2048, 8192):
+        for kind, name in probes:
             ts = []
             for _ in range(a.rounds):
                 e0.record()
                 for _ in range(a.iters):
-                    ext.hip.bandwidth_probe(kind, f0.data_ptr(), f1.data_ptr() if kind == 0 else sink.data_ptr(),
+                    ext.hip.bandwidth_probe(kind, f0.data_ptr(), f1.data_ptr() if kind != 1 else sink.data_ptr(),
                                             nbytes, blocks, strm)
                 e1.record()
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1) / a.iters)
-            moved = nbytes * (2 if kind == 0 else 1)
+            moved = nbytes * (2 if kind != 1 else 1)
             print(json.dumps({"probe": name, "blocks": blocks, "bytes": moved,
                               "tbps": round(moved / (statistics.median(ts) * 1e-3) / 1e12, 3)}), flush=True)
     out = []
