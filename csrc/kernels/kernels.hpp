@@ -16,7 +16,7 @@
 namespace heat3d {
 
 struct KernelSpec {
-  enum Kind { Naive = 0, Column = 1, Tile = 2 } kind = Column;
+  enum Kind { Naive = 0, Column = 1, Tile = 2 } kind = Tile;
   int WZ = 0, WY = 0;  // tile kernel: waves per workgroup along z and y
   int V = 0;  // elements per lane along z (0 = default for dtype)
   int R = 0;  // rows per wave along y (0 = default)

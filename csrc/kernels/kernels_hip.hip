@@ -478,10 +478,14 @@ static void launch_tile(const StencilParams& p, const KernelSpec& k, hipStream_t
   g.nyb = (int)((b.extent(1) + (int64_t)R * WY - 1) / ((int64_t)R * WY));
   int seg = k.L;
   if (seg <= 0) {
-    // ~8 resident rounds of 256 CUs; segments no shorter than 16 planes
+    // Every x segment re-reads two planes, so segments should be long; but the
+    // grid needs several workgroups per CU.  Aim for ~2048 workgroups with
+    // segments of at least 32 planes (>= 512 workgroups whenever possible).
     const int64_t tiles = (int64_t)g.nzb * g.nyb;
     const int64_t want = std::max<int64_t>(1, 2048 / std::max<int64_t>(1, tiles));
-    seg = (int)std::max<int64_t>(16, (b.extent(0) + want - 1) / want);
+    seg = (int)((b.extent(0) + want - 1) / want);
+    const int64_t min_seg = std::min<int64_t>(32, std::max<int64_t>(1, b.extent(0) * tiles / 512));
+    seg = (int)std::max<int64_t>(seg, std::max<int64_t>(16, min_seg));
   }
   g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));
   g.nxs = (int)((b.extent(0) + g.seg - 1) / g.seg);
@@ -575,9 +579,11 @@ static void dispatch_column(const StencilParams& p, const KernelSpec& k, hipStre
 
 template <typename Real>
 static void dispatch_tile(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
+  // defaults from the gfx950 sweep (profiles/kernel_sweep.md): 8-wave tiles,
+  // 16 rows x 512 points fp64, 16 rows x 512 points fp32
   const int V = k.V ? k.V : (sizeof(Real) == 8 ? 2 : 4);
   const int R = k.R ? k.R : 8;
-  const int WZ = k.WZ ? k.WZ : 2, WY = k.WY ? k.WY : 2;
+  const int WZ = k.WZ ? k.WZ : (sizeof(Real) == 8 ? 4 : 2), WY = k.WY ? k.WY : 2;
   if (p.box.extent(2) < 32 || p.box.extent(1) < 2) {
     launch_naive<Real>(p, s);
     return;
@@ -589,7 +595,7 @@ static void dispatch_tile(const StencilParams& p, const KernelSpec& k, hipStream
   }
   H3D_TILE(2, 4, 1, 4) H3D_TILE(2, 4, 2, 2) H3D_TILE(2, 4, 2, 4) H3D_TILE(2, 4, 4, 2)
   H3D_TILE(2, 8, 1, 4) H3D_TILE(2, 8, 2, 2) H3D_TILE(2, 8, 4, 1) H3D_TILE(2, 8, 2, 4)
-  H3D_TILE(2, 8, 4, 2) H3D_TILE(2, 6, 2, 2) H3D_TILE(2, 6, 2, 4)
+  H3D_TILE(2, 8, 4, 2) H3D_TILE(2, 6, 2, 2) H3D_TILE(2, 6, 2, 4) H3D_TILE(2, 8, 8, 1)
   if constexpr (sizeof(Real) == 4) {
     H3D_TILE(4, 4, 2, 2) H3D_TILE(4, 8, 2, 2) H3D_TILE(4, 8, 1, 4) H3D_TILE(4, 4, 2, 4)
   }
