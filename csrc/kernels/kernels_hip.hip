@@ -466,6 +466,44 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tile(const Real* __restr
   if (res) residual_commit(res, m);
 }
 
+// Resident workgroups of `kernel` on the whole device (occupancy x CUs).
+static int device_slots(const void* kernel, int block) {
+  int dev = 0, cus = 256, per = 1;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess || per < 1) per = 1;
+  return std::max(1, cus * per);
+}
+
+// x-segment length for an x-marching kernel.  Each segment re-reads two
+// planes, and the grid runs in ceil(blocks / slots) rounds, so the sweep costs
+// ~ rounds * (seg + 2) plane-steps per slot.  Take the cheapest segment; among
+// near-ties prefer more rounds (dynamic balance), up to 8.
+static int choose_segment(int64_t nx, int64_t tiles, int slots) {
+  if (nx <= 1) return 1;
+  double best = 1e300;
+  std::vector<std::pair<double, int>> c;
+  for (int64_t parts = 1; parts <= std::min<int64_t>(nx, 512); ++parts) {
+    const int64_t seg = (nx + parts - 1) / parts;
+    const int64_t nxs = (nx + seg - 1) / seg;
+    const int64_t rounds = (tiles * nxs + slots - 1) / slots;
+    const double cost = (double)rounds * (double)(seg + 2);
+    c.push_back({cost, (int)seg});
+    best = std::min(best, cost);
+  }
+  int pick = (int)nx, pick_rounds = 0;
+  for (auto& e : c) {
+    if (e.first > best * 1.03) continue;
+    const int64_t nxs = (nx + e.second - 1) / e.second;
+    const int rounds = (int)((tiles * nxs + slots - 1) / slots);
+    if (rounds <= 8 && rounds > pick_rounds) {
+      pick_rounds = rounds;
+      pick = e.second;
+    }
+  }
+  return std::max(1, pick);
+}
+
 template <typename Real, int V, int R, int WZ, int WY>
 static void launch_tile(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
   const Box& b = p.box;
@@ -478,14 +516,10 @@ static void launch_tile(const StencilParams& p, const KernelSpec& k, hipStream_t
   g.nyb = (int)((b.extent(1) + (int64_t)R * WY - 1) / ((int64_t)R * WY));
   int seg = k.L;
   if (seg <= 0) {
-    // Every x segment re-reads two planes, so segments should be long; but the
-    // grid needs several workgroups per CU.  Aim for ~2048 workgroups with
-    // segments of at least 32 planes (>= 512 workgroups whenever possible).
-    const int64_t tiles = (int64_t)g.nzb * g.nyb;
-    const int64_t want = std::max<int64_t>(1, 2048 / std::max<int64_t>(1, tiles));
-    seg = (int)((b.extent(0) + want - 1) / want);
-    const int64_t min_seg = std::min<int64_t>(32, std::max<int64_t>(1, b.extent(0) * tiles / 512));
-    seg = (int)std::max<int64_t>(seg, std::max<int64_t>(16, min_seg));
+    static int slots = 0;  // resident workgroups on the whole device (cached per instantiation)
+    if (!slots) slots = device_slots(reinterpret_cast<const void*>(&stencil_tile<Real, V, R, WZ, WY>),
+                                     64 * WZ * WY);
+    seg = choose_segment(b.extent(0), (int64_t)g.nzb * g.nyb, slots);
   }
   g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));
   g.nxs = (int)((b.extent(0) + g.seg - 1) / g.seg);
