@@ -55,6 +55,11 @@ int main(int argc, char** argv) {
                     solver->kernel_name().c_str(), (long long)r.iterations, (long long)r.issued,
                     r.glups, r.norm, r.last_residual);
       }
+      if (cfg.timers) {
+        std::printf("heat3d: phase timing (ms/iteration, synchronised):");
+        for (auto& pt : solver->phase_times()) std::printf(" %s=%.4f", pt.first.c_str(), pt.second);
+        std::printf("\n");
+      }
       if (r.fault) std::fprintf(stderr, "heat3d: non-finite residual detected at iteration %lld\n",
                                 (long long)r.conv_iter);
       std::fflush(stdout);

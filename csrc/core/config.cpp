@@ -94,6 +94,8 @@ std::string Config::usage() {
      << "  --checkpoint-every K --checkpoint-dir DIR   periodic binary checkpoints\n"
      << "  --restart DIR             resume from a checkpoint directory\n"
      << "  --json-out PATH           write a JSON run report\n"
+     << "  --verify-halo K           race detection: checksum every halo face every K iterations\n"
+     << "  --timers                  per-phase GPU timing (synchronised diagnostic run)\n"
      << "  --verbose N               print residual every N iterations\n"
      << "  --threads N               CPU backend OpenMP threads\n"
      << "  --quiet                   suppress the banner\n";
@@ -171,6 +173,8 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--tecplot-layout") c.tecplot_layout = get("--tecplot-layout");
     else if (key == "--compat") c.compat = true;
     else if (key == "--checkpoint-every") c.checkpoint_every = to_i64(get("--checkpoint-every"), "--checkpoint-every");
+    else if (key == "--verify-halo") c.verify_halo = to_i64(get("--verify-halo"), "--verify-halo");
+    else if (key == "--timers") c.timers = true;
     else if (key == "--checkpoint-dir") c.checkpoint_dir = get("--checkpoint-dir");
     else if (key == "--restart") c.restart = get("--restart");
     else if (key == "--json-out") c.json_out = get("--json-out");

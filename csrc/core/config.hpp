@@ -54,6 +54,8 @@ struct Config {
   std::string tecplot_layout = "auto";    // auto | ref | owned
   bool compat = false;                    // reproduce reference reporting quirks
   int64_t checkpoint_every = 0;
+  int64_t verify_halo = 0;                // race detection: checksum halos every K iterations
+  bool timers = false;                    // per-phase timing (synchronised diagnostic run)
   std::string checkpoint_dir;
   std::string restart;
   std::string json_out;

@@ -73,6 +73,9 @@ int64_t error_scratch_elems();
 // Fault injection (tests): write `value` at local owned point (i,j,k).
 void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k, double value,
           void* stream);
+// Order-independent checksum (sum of bit patterns mod 2^64) of a box -> *out (device).
+void box_bitsum(DType t, const void* f, const Layout& L, const Box& b, unsigned long long* out,
+                void* stream);
 // HBM calibration: kind 0 = 16 B/lane copy src->dst, 1 = 16 B/lane read of src.
 void bandwidth_probe(int kind, const void* src, void* dst, int64_t bytes, int blocks, void* stream);
 }  // namespace hip
@@ -89,6 +92,7 @@ void check_convergence(DeviceState* s, int slot);
 void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
                       const int64_t gstart[3], double hy, DeviceState* s);
 void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k, double value);
+unsigned long long box_bitsum(DType t, const void* f, const Layout& L, const Box& b);
 }  // namespace cpu
 
 // Shared scalar logic of the convergence check (heat3D.cu:1026-1073 with the

@@ -181,6 +181,25 @@ void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
   else error_t(static_cast<const float*>(f), L, box, gstart, hy, s);
 }
 
+unsigned long long box_bitsum(DType t, const void* f, const Layout& L, const Box& b) {
+  unsigned long long acc = 0;
+  for (int64_t i = b.lo[0]; i < b.hi[0]; ++i)
+    for (int64_t j = b.lo[1]; j < b.hi[1]; ++j)
+      for (int64_t k = b.lo[2]; k < b.hi[2]; ++k) {
+        const int64_t q = L.index(i, j, k);
+        if (t == DType::F64) {
+          unsigned long long u;
+          std::memcpy(&u, static_cast<const double*>(f) + q, 8);
+          acc += u;
+        } else {
+          unsigned u;
+          std::memcpy(&u, static_cast<const float*>(f) + q, 4);
+          acc += u;
+        }
+      }
+  return acc;
+}
+
 void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k, double value) {
   if (t == DType::F64) static_cast<double*>(f)[L.index(i, j, k)] = value;
   else static_cast<float*>(f)[L.index(i, j, k)] = static_cast<float>(value);

@@ -477,28 +477,21 @@ static int device_slots(const void* kernel, int block) {
 
 // x-segment length for an x-marching kernel.  Each segment re-reads two
 // planes, and the grid runs in ceil(blocks / slots) rounds, so the sweep costs
-// ~ rounds * (seg + 2) plane-steps per slot.  Take the cheapest segment; among
-// near-ties prefer more rounds (dynamic balance), up to 8.
+// ~ rounds * (seg + 2) plane-steps per slot.  Take the cheapest segment (ties:
+// the longer one).  Measured on MI355X, 1024^3 fp64: 1 round of 511-plane
+// segments 321 GLUPS vs 8 rounds of 64 planes 313 (profiles/kernel_sweep.md).
 static int choose_segment(int64_t nx, int64_t tiles, int slots) {
   if (nx <= 1) return 1;
   double best = 1e300;
-  std::vector<std::pair<double, int>> c;
+  int pick = (int)nx;
   for (int64_t parts = 1; parts <= std::min<int64_t>(nx, 512); ++parts) {
     const int64_t seg = (nx + parts - 1) / parts;
     const int64_t nxs = (nx + seg - 1) / seg;
     const int64_t rounds = (tiles * nxs + slots - 1) / slots;
     const double cost = (double)rounds * (double)(seg + 2);
-    c.push_back({cost, (int)seg});
-    best = std::min(best, cost);
-  }
-  int pick = (int)nx, pick_rounds = 0;
-  for (auto& e : c) {
-    if (e.first > best * 1.03) continue;
-    const int64_t nxs = (nx + e.second - 1) / e.second;
-    const int rounds = (int)((tiles * nxs + slots - 1) / slots);
-    if (rounds <= 8 && rounds > pick_rounds) {
-      pick_rounds = rounds;
-      pick = e.second;
+    if (cost < best - 1e-9) {
+      best = cost;
+      pick = (int)seg;
     }
   }
   return std::max(1, pick);
@@ -791,6 +784,40 @@ void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
   HIPK_CHECK(hipGetLastError());
   hipLaunchKernelGGL(error_final_kernel, dim3(1), dim3(64), 0, S(stream), scratch, kErrBlocks,
                      (double)box.volume(), s);
+  HIPK_CHECK(hipGetLastError());
+}
+
+// ---- halo verification: order-independent checksum of a box -------------------
+// Sum (mod 2^64) of the values' bit patterns: exact and independent of the
+// summation order, so sender and receiver of a halo can compare checksums.
+template <typename Real>
+__global__ __launch_bounds__(256) void bitsum_kernel(const Real* f, Layout L, Box b,
+                                                     unsigned long long* out) {
+  const int64_t ey = b.extent(1), ez = b.extent(2);
+  const int64_t n = b.extent(0) * ey * ez;
+  unsigned long long acc = 0;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256) {
+    const int64_t k = q % ez, j = (q / ez) % ey, i = q / (ez * ey);
+    const Real v = f[L.index(b.lo[0] + i, b.lo[1] + j, b.lo[2] + k)];
+    if constexpr (sizeof(Real) == 8) acc += (unsigned long long)__builtin_bit_cast(long long, v);
+    else acc += (unsigned long long)(unsigned)__builtin_bit_cast(int, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+void box_bitsum(DType t, const void* f, const Layout& L, const Box& b, unsigned long long* out,
+                void* stream) {
+  HIPK_CHECK(hipMemsetAsync(out, 0, 8, S(stream)));
+  if (b.empty()) return;
+  const int blocks = (int)std::min<int64_t>(1024, (b.volume() + 255) / 256);
+  if (t == DType::F64)
+    hipLaunchKernelGGL(bitsum_kernel<double>, dim3(blocks), dim3(256), 0, S(stream),
+                       static_cast<const double*>(f), L, b, out);
+  else
+    hipLaunchKernelGGL(bitsum_kernel<float>, dim3(blocks), dim3(256), 0, S(stream),
+                       static_cast<const float*>(f), L, b, out);
   HIPK_CHECK(hipGetLastError());
 }
 

@@ -370,7 +370,12 @@ PYBIND11_MODULE(_heat3d, m) {
         py::gil_scoped_release nogil;
         s.load_checkpoint(d);
       })
-      .def("inject", &Solver::inject)
+      .def("inject", &Solver::inject, py::arg("idx"), py::arg("i"), py::arg("j"), py::arg("k"),
+           py::arg("value"), py::arg("previous") = false)
+      .def("verify_halos", [](Solver& s) {
+        py::gil_scoped_release nogil;
+        return s.verify_halos();
+      })
       .def("set_phase_timing", &Solver::set_phase_timing)
       .def("phase_times", &Solver::phase_times)
       .def_property_readonly("num_local", &Solver::num_local)

@@ -70,6 +70,9 @@ class Backend {
                                 StreamId s) = 0;
   virtual void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k,
                     double value, StreamId s) = 0;
+  // order-independent checksum of a box into *out (device memory on HIP)
+  virtual void box_bitsum(DType t, const void* f, const Layout& L, const Box& b,
+                          unsigned long long* out, StreamId s) = 0;
   // tracing ranges (roctx on HIP)
   virtual void range_push(const char* /*name*/) {}
   virtual void range_pop() {}

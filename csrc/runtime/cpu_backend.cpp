@@ -71,6 +71,10 @@ class CpuBackend final : public Backend {
             StreamId) override {
     cpu::poke(t, f, L, i, j, k, value);
   }
+  void box_bitsum(DType t, const void* f, const Layout& L, const Box& b, unsigned long long* out,
+                  StreamId) override {
+    *out = cpu::box_bitsum(t, f, L, b);
+  }
 };
 
 }  // namespace

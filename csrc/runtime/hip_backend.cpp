@@ -180,6 +180,10 @@ class HipBackend final : public Backend {
             StreamId s) override {
     hip::poke(t, f, L, i, j, k, value, streams_[s]);
   }
+  void box_bitsum(DType t, const void* f, const Layout& L, const Box& b, unsigned long long* out,
+                  StreamId s) override {
+    hip::box_bitsum(t, f, L, b, out, streams_[s]);
+  }
   void range_push(const char* n) override {
     if (roctx_.push) roctx_.push(n);
   }

@@ -109,6 +109,8 @@ Solver::~Solver() {
   for (auto& e : ev_)
     if (e) be_->event_destroy(e);
   for (auto& e : cap_pool_) be_->event_destroy(e);
+  for (auto& e : tev_)
+    if (e) be_->event_destroy(e);
   for (auto& l : local_) {
     for (auto* f : l.field) be_->release(f);
     for (auto& io : l.faces) {
@@ -306,37 +308,64 @@ void Solver::enqueue_iteration(int p) {
     sp.slot = p;
     return sp;
   };
+  // per-phase timer events (diagnostic mode: one synchronised iteration at a time)
+  auto T = [&](int i, StreamId s) {
+    if (phase_timing_) be_->record(tev_[i], s);
+  };
   // [A] interior sweep on the compute stream
   ev_wait(kCompute, EV_CHK + p);  // convergence check of iteration t-2 (flag + slot reset)
+  T(0, kCompute);
   if (overlap_) {
     ev_wait(kCompute, EV_BND + (p ^ 1));  // shell of t-1 written (and read) before we overwrite
     be_->range_push("interior");
     for (auto& l : local_) be_->stencil(dt_, params(l, l.interior), kspec_, kCompute);
     be_->range_pop();
+    T(1, kCompute);
     ev_record(EV_INT + p, kCompute);
     // [B] halo exchange + shell on the comm stream
     ev_wait(kComm, EV_INT + (p ^ 1));  // interior of t-1 done (RAW on layer 1, WAR on shell)
     ev_wait(kComm, EV_CHK + p);
+    T(2, kComm);
     enqueue_halo(p);
+    T(3, kComm);
     be_->range_push("shell");
     for (auto& l : local_)
       for (const Box& b : l.shell) be_->stencil(dt_, params(l, b), kspec_, kComm);
     be_->range_pop();
+    T(4, kComm);
     ev_record(EV_BND + p, kComm);
   } else {
+    T(2, kCompute);
     if (has_halo_) enqueue_halo(p);
+    T(3, kCompute);
     be_->range_push("sweep");
     for (auto& l : local_) be_->stencil(dt_, params(l, l.owned), kspec_, kCompute);
     be_->range_pop();
+    T(1, kCompute);
+    T(4, kCompute);
     ev_record(EV_INT + p, kCompute);
   }
   // [C] global residual + convergence check on the reduce stream
   ev_wait(kReduce, EV_INT + p);
   if (overlap_) ev_wait(kReduce, EV_BND + p);
+  T(5, kReduce);
   if (!comm_->all_local() && comm_->size() > 1)
     comm_->allreduce(&dstate_->residual[p], 1, RedType::U64, RedOp::Max, *be_, kReduce);
   be_->check_convergence(dstate_, p, kReduce);
+  T(6, kReduce);
   ev_record(EV_CHK + p, kReduce);
+}
+
+void Solver::accumulate_phase_times() {
+  be_->sync_all();
+  static const char* names[] = {"interior_ms", "halo_ms", "shell_ms", "reduce_check_ms", "iteration_ms"};
+  const double v[5] = {be_->elapsed_ms(tev_[0], tev_[1]), be_->elapsed_ms(tev_[2], tev_[3]),
+                       be_->elapsed_ms(tev_[3], tev_[4]), be_->elapsed_ms(tev_[5], tev_[6]),
+                       be_->elapsed_ms(tev_[0], tev_[6])};
+  if (phase_acc_.empty())
+    for (auto* n : names) phase_acc_.push_back({n, 0.0});
+  for (int i = 0; i < 5; ++i) phase_acc_[i].second += v[i];
+  ++phase_count_;
 }
 
 void Solver::build_graph() {
@@ -412,17 +441,10 @@ void Solver::run_chunk(int64_t n) {
         continue;
       }
     }
-    if (phase_timing_) {
-      ev_record(EV_T0, kCompute);
-    }
+    if (phase_timing_ && !tev_[0])
+      for (auto& e : tev_) e = be_->event_create();
     enqueue_iteration((int)(issued_ & 1));
-    if (phase_timing_) {
-      ev_record(EV_T1, kReduce);
-      be_->event_sync(cur_ev_[EV_T1]);
-      double ms = be_->elapsed_ms(cur_ev_[EV_T0], cur_ev_[EV_T1]);
-      if (phase_acc_.empty()) phase_acc_.push_back({"iteration_ms", 0.0});
-      phase_acc_[0].second += ms;
-    }
+    if (phase_timing_) accumulate_phase_times();
     ++issued_;
     --n;
   }
@@ -464,6 +486,8 @@ RunResult Solver::run() {
   int pslot = 0;
   bool have_prev = false, stop = false;
   int64_t next_ckpt = cfg_.checkpoint_every > 0 ? issued_ + cfg_.checkpoint_every : -1;
+  int64_t next_verify = cfg_.verify_halo > 0 ? issued_ + cfg_.verify_halo : -1;
+  if (cfg_.timers) set_phase_timing(true);
   int64_t printed = issued_;
   const double watchdog = std::getenv("HEAT3D_WATCHDOG_S") ? std::atof(std::getenv("HEAT3D_WATCHDOG_S")) : 900.0;
   while (issued_ < cfg_.iter_max && !stop) {
@@ -499,6 +523,14 @@ RunResult Solver::run() {
       HostState hs = state();
       if (!hs.done) save_checkpoint(cfg_.checkpoint_dir.empty() ? "checkpoint" : cfg_.checkpoint_dir);
       next_ckpt = issued_ + cfg_.checkpoint_every;
+    }
+    if (cfg_.verify_halo > 0 && issued_ >= next_verify) {
+      const int bad = verify_halos();
+      if (bad) {
+        comm_->abort();
+        HEAT3D_THROW("halo verification failed on " << bad << " face(s) after iteration " << issued_);
+      }
+      next_verify = issued_ + cfg_.verify_halo;
     }
   }
   be_->sync_all();
@@ -768,12 +800,90 @@ void Solver::load_checkpoint(const std::string& dir) {
   issued_ = it;
 }
 
-std::vector<std::pair<std::string, double>> Solver::phase_times() { return phase_acc_; }
+int Solver::verify_halos() {
+  be_->sync_all();
+  if (issued_ == 0 || !has_halo_) return 0;
+  // input buffer of the last iteration: its ghosts were filled by that
+  // iteration's exchange from the neighbours' (unchanged) faces
+  const int p = (int)((issued_ - 1) & 1);
+  int nf = 0;
+  for (auto& l : local_) nf += (int)l.faces.size();
+  auto* dsum = static_cast<unsigned long long*>(be_->alloc(sizeof(unsigned long long) * 3 * nf));
+  int q = 0;
+  for (auto& l : local_)
+    for (auto& io : l.faces) {
+      be_->box_bitsum(dt_, l.field[p], l.L, io.send_box, dsum + 2 * q, kCompute);
+      be_->box_bitsum(dt_, l.field[p], l.L, io.recv_box, dsum + 2 * q + 1, kCompute);
+      ++q;
+    }
+  be_->sync(kCompute);
+  std::vector<unsigned long long> h(3 * nf, 0);
+  int bad = 0;
+  if (comm_->all_local()) {
+    be_->copy(h.data(), dsum, sizeof(unsigned long long) * 2 * nf, CopyKind::D2H, kCompute);
+    be_->sync(kCompute);
+    std::vector<int> base(local_.size(), 0);
+    for (std::size_t i = 1; i < local_.size(); ++i) base[i] = base[i - 1] + (int)local_[i - 1].faces.size();
+    for (std::size_t i = 0; i < local_.size(); ++i)
+      for (std::size_t f = 0; f < local_[i].faces.size(); ++f) {
+        const auto& io = local_[i].faces[f];
+        const auto& nb = local_[io.peer_local];
+        for (std::size_t g = 0; g < nb.faces.size(); ++g)
+          if (nb.faces[g].face == opposite(io.face) && h[2 * (base[io.peer_local] + g)] != h[2 * (base[i] + f) + 1]) {
+            std::fprintf(stderr, "heat3d: halo mismatch rank %d face %s\n", local_[i].sd.rank, face_name(io.face));
+            ++bad;
+          }
+      }
+  } else {
+    // send my send-box checksum to each neighbour, receive theirs
+    std::vector<Transfer> xs;
+    q = 0;
+    for (auto& l : local_)
+      for (auto& io : l.faces) {
+        Transfer s, r;
+        s.src_rank = l.sd.rank;
+        s.dst_rank = io.peer;
+        s.src = dsum + 2 * q;
+        s.bytes = 8;
+        r.src_rank = io.peer;
+        r.dst_rank = l.sd.rank;
+        r.dst = dsum + 2 * nf + q;
+        r.bytes = 8;
+        xs.push_back(s);
+        xs.push_back(r);
+        ++q;
+      }
+    comm_->exchange(xs, *be_, kCompute);
+    be_->sync(kCompute);
+    be_->copy(h.data(), dsum, sizeof(unsigned long long) * 3 * nf, CopyKind::D2H, kCompute);
+    be_->sync(kCompute);
+    q = 0;
+    for (auto& l : local_)
+      for (auto& io : l.faces) {
+        if (h[2 * nf + q] != h[2 * q + 1]) {
+          std::fprintf(stderr, "heat3d: halo mismatch rank %d face %s (peer %d)\n", l.sd.rank,
+                       face_name(io.face), io.peer);
+          ++bad;
+        }
+        ++q;
+      }
+  }
+  be_->release(dsum);
+  return bad;
+}
 
-void Solver::inject(int idx, int64_t i, int64_t j, int64_t k, double value) {
+std::vector<std::pair<std::string, double>> Solver::phase_times() {
+  std::vector<std::pair<std::string, double>> out = phase_acc_;
+  for (auto& e : out) e.second /= std::max<int64_t>(1, phase_count_);
+  return out;
+}
+
+void Solver::inject(int idx, int64_t i, int64_t j, int64_t k, double value, bool previous) {
   be_->sync_all();
   auto& l = local_.at(idx);
-  be_->poke(dt_, l.field[issued_ & 1], l.L, i, j, k, value, kCompute);
+  HEAT3D_CHECK(i >= -1 && i <= l.sd.n[0] && j >= -1 && j <= l.sd.n[1] && k >= -1 && k <= l.sd.n[2],
+               "inject index outside the ghosted block");
+  be_->poke(dt_, l.field[(issued_ + (previous ? 1 : 0)) & 1], l.L, i, j, k, value, kCompute);
   be_->sync(kCompute);
 }
 

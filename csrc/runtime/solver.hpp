@@ -103,11 +103,22 @@ class Solver {
   void load_checkpoint(const std::string& dir);
 
   // Per-phase timing (ms, averaged over timed iterations) when enabled.
-  void set_phase_timing(bool on) { phase_timing_ = on; }
+  // Diagnostic: every iteration is synchronised, graphs are off.
+  void set_phase_timing(bool on) {
+    phase_timing_ = on;
+    phase_acc_.clear();
+    phase_count_ = 0;
+  }
   std::vector<std::pair<std::string, double>> phase_times();
 
+  // Race detection: compare order-independent checksums of every face sent
+  // in the last exchange with the ghost layer the neighbour received.
+  // Returns the number of mismatching faces (0 = consistent).
+  int verify_halos();
+
   // Fault injection for tests: write `value` into a local owned point.
-  void inject(int local_idx, int64_t i, int64_t j, int64_t k, double value);
+  // `previous` targets the other ping-pong buffer (the last iteration's input).
+  void inject(int local_idx, int64_t i, int64_t j, int64_t k, double value, bool previous = false);
 
  private:
   struct FaceIO {
@@ -172,6 +183,9 @@ class Solver {
 
   bool phase_timing_ = false;
   std::vector<std::pair<std::string, double>> phase_acc_;
+  int64_t phase_count_ = 0;
+  Event tev_[8] = {};
+  void accumulate_phase_times();
 };
 
 // Build a Solver for a parsed command line in this process: chooses backend,

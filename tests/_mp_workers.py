@@ -31,6 +31,7 @@ def native_socket_worker(rank, world, port, outdir, n, eps, decomp, dtype):
                               threads=2)
     assert s.native.comm_name == "socket"
     r = s.run()
+    assert s.native.verify_halos() == 0  # checksums exchanged over the socket transport
     g = s.gather()
     ck = os.path.join(outdir, "ckpt")
     s.save_checkpoint(ck)

@@ -134,3 +134,25 @@ def test_model_matches_native_init(h3d):
     for p in [(0, 3, 4), (3, 9, 4), (8, 0, 10), (4, 4, 4)]:
         assert ext.boundary_value(*p, list(m.n), list(m.h)) == (m.boundary_value(*p) if
                                                                0 in p or p[0] == 8 or p[1] == 9 or p[2] == 10 else 0.0)
+
+
+@pytest.mark.parametrize("vr,decomp", [(2, (2, 1, 1)), (8, (2, 2, 2))])
+def test_verify_halos_detects_corruption(h3d, vr, decomp):
+    s = h3d.HeatSolver((19, 19, 19), 10 ** 6, 0.0, backend="cpu", virtual_ranks=vr, decomp=decomp)
+    s.initialize()
+    s.step(7)
+    assert s.native.verify_halos() == 0
+    # corrupt one ghost value of subdomain 0 in the buffer the check inspects
+    sub = s.native.local_subdomain(0)
+    s.native.inject(0, sub["n"][0], 2, 3, 123.0, previous=True)
+    assert s.native.verify_halos() >= 1
+
+
+def test_phase_timers(h3d):
+    s = h3d.HeatSolver((33, 33, 33), 100, 0.0, backend="cpu", virtual_ranks=4)
+    s.initialize()
+    s.native.set_phase_timing(True)
+    s.step(5)
+    t = dict(s.native.phase_times())
+    assert set(t) == {"interior_ms", "halo_ms", "shell_ms", "reduce_check_ms", "iteration_ms"}
+    assert t["iteration_ms"] >= t["interior_ms"] >= 0
