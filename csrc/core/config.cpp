@@ -87,7 +87,10 @@ std::string Config::usage() {
      << "  --graph / --no-graph      capture iterations in hipGraphs (default on)\n"
      << "  --no-overlap              do not split interior/boundary work\n"
      << "  --check-every K           host poll period of the device convergence flag\n"
-     << "  --kernel NAME             stencil kernel variant (auto|naive|column[:V:R:L])\n"
+     << "  --kernel NAME             stencil kernel variant (auto|tile[:V:R:WZ:WY:L]|column|naive)\n"
+     << "  --temporal 0|1|2          2-step temporal blocking (0 auto: on for one halo-free GPU\n"
+     << "                            subdomain; results are bitwise identical)\n"
+     << "  --kernel2 tb2[:V:R:WZ:WY:L]  temporally blocked kernel variant\n"
      << "  --output PATH|none        Tecplot output (default output/out.dat for small grids)\n"
      << "  --tecplot-layout auto|ref|owned\n"
      << "  --compat                  reproduce reference reporting quirks\n"
@@ -169,6 +172,11 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--check-every") c.check_every = (int)to_i64(get("--check-every"), "--check-every");
     else if (key == "--graph-chunk") c.graph_chunk = (int)to_i64(get("--graph-chunk"), "--graph-chunk");
     else if (key == "--kernel") c.kernel = get("--kernel");
+    else if (key == "--kernel2") c.kernel2 = get("--kernel2");
+    else if (key == "--temporal") {
+      c.temporal = (int)to_i64(get("--temporal"), "--temporal");
+      if (c.temporal < 0 || c.temporal > 2) throw UsageError("--temporal must be 0 (auto), 1 or 2");
+    }
     else if (key == "--output") c.output = get("--output");
     else if (key == "--tecplot-layout") c.tecplot_layout = get("--tecplot-layout");
     else if (key == "--compat") c.compat = true;

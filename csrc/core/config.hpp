@@ -50,6 +50,8 @@ struct Config {
   int check_every = 64;                   // host poll period for the device convergence flag
   int graph_chunk = 32;                   // iterations per captured hipGraph (rounded to even)
   std::string kernel = "auto";            // stencil kernel variant
+  std::string kernel2 = "auto";           // 2-step temporally blocked kernel variant
+  int temporal = 0;                       // 0 auto (2 on GPU without halos), 1 off, 2 on
   std::string output = "auto";            // path | none | auto (output/out.dat when small)
   std::string tecplot_layout = "auto";    // auto | ref | owned
   bool compat = false;                    // reproduce reference reporting quirks

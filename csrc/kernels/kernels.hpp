@@ -16,7 +16,7 @@
 namespace heat3d {
 
 struct KernelSpec {
-  enum Kind { Naive = 0, Column = 1, Tile = 2 } kind = Tile;
+  enum Kind { Naive = 0, Column = 1, Tile = 2, TB2 = 3 } kind = Tile;
   int WZ = 0, WY = 0;  // tile kernel: waves per workgroup along z and y
   int V = 0;  // elements per lane along z (0 = default for dtype)
   int R = 0;  // rows per wave along y (0 = default)
@@ -59,6 +59,10 @@ H3D_HD inline double boundary_value(int64_t gi, int64_t gj, int64_t gk, const in
 namespace hip {
 void init_field(DType t, const InitParams& p, void* stream);
 void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+// Two FTCS steps in one sweep (stencil_tb2.hip): p.in = T^n, p.out = T^{n+2};
+// residuals of the two steps go to slots p.slot and p.slot ^ 1.  The box must
+// be a whole subdomain whose ghosts are constant (Dirichlet) values.
+void stencil2(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, void* stream);
 void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, void* stream);
 void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,

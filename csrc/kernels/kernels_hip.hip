@@ -30,93 +30,10 @@
 #include <cstdio>
 #include <cstring>
 
-#include "kernels.hpp"
-
-#pragma clang fp contract(off)
+#include "hip_helpers.hpp"
 
 namespace heat3d {
 namespace hip {
-
-#define HIPK_CHECK(expr)                                                             \
-  do {                                                                               \
-    hipError_t _e = (expr);                                                          \
-    if (_e != hipSuccess) HEAT3D_THROW("HIP error " << hipGetErrorString(_e) << " at " #expr); \
-  } while (0)
-
-static inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
-
-template <typename Real, int V>
-struct VecOf;
-template <> struct VecOf<double, 1> { typedef double type; };
-template <> struct VecOf<double, 2> { typedef double type __attribute__((ext_vector_type(2))); };
-template <> struct VecOf<float, 1> { typedef float type; };
-template <> struct VecOf<float, 2> { typedef float type __attribute__((ext_vector_type(2))); };
-template <> struct VecOf<float, 4> { typedef float type __attribute__((ext_vector_type(4))); };
-
-template <typename Real>
-__device__ __forceinline__ Real ftcs(Real c, Real xm, Real xp, Real ym, Real yp, Real zm, Real zp,
-                                     Real Dx, Real Dy, Real Dz) {
-#pragma clang fp contract(off)
-  const Real c2 = Real(2) * c;
-  const Real ax = (xp - c2) + xm;
-  const Real ay = (yp - c2) + ym;
-  const Real az = (zp - c2) + zm;
-  return ((c + Dx * ax) + Dy * ay) + Dz * az;
-}
-
-// ---- cross-lane helpers ----------------------------------------------------
-// DPP wave_shr:1 (0x138): lane i <- lane i-1 ; lane 0 keeps `old`.
-// DPP wave_shl:1 (0x130): lane i <- lane i+1 ; lane 63 keeps `old`.
-__device__ __forceinline__ double dpp_shr1(double old, double v) {
-  long long ov = __builtin_bit_cast(long long, old), vv = __builtin_bit_cast(long long, v);
-  int lo = __builtin_amdgcn_update_dpp((int)ov, (int)vv, 0x138, 0xf, 0xf, false);
-  int hi = __builtin_amdgcn_update_dpp((int)(ov >> 32), (int)(vv >> 32), 0x138, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double dpp_shl1(double old, double v) {
-  long long ov = __builtin_bit_cast(long long, old), vv = __builtin_bit_cast(long long, v);
-  int lo = __builtin_amdgcn_update_dpp((int)ov, (int)vv, 0x130, 0xf, 0xf, false);
-  int hi = __builtin_amdgcn_update_dpp((int)(ov >> 32), (int)(vv >> 32), 0x130, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ float dpp_shr1(float old, float v) {
-  int r = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
-                                      0x138, 0xf, 0xf, false);
-  return __builtin_bit_cast(float, r);
-}
-__device__ __forceinline__ float dpp_shl1(float old, float v) {
-  int r = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
-                                      0x130, 0xf, 0xf, false);
-  return __builtin_bit_cast(float, r);
-}
-__device__ __forceinline__ double readlane(double v, int lane) {
-  long long b = __builtin_bit_cast(long long, v);
-  int lo = __builtin_amdgcn_readlane((int)b, lane);
-  int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ float readlane(float v, int lane) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
-}
-
-// Residual max over non-negative doubles, done on their IEEE bit patterns:
-// integer order == double order, and a NaN (bits above +Inf) wins, so a
-// blown-up field reaches the convergence check as a fault.
-__device__ __forceinline__ double res_max(double m, double d) { return (d != d || d > m) ? d : m; }
-
-__device__ __forceinline__ void residual_commit(unsigned long long* slot, double m) {
-  unsigned long long b = (unsigned long long)__builtin_bit_cast(long long, m);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    unsigned long long q = __shfl_xor(b, o, 64);
-    b = q > b ? q : b;
-  }
-  if ((threadIdx.x & 63) == 0) atomicMax(slot, b);
-}
-
-__device__ __forceinline__ bool flag_set(const int* done) {
-  return done != nullptr && __builtin_nontemporal_load(done) != 0;
-}
 
 // ---- naive kernel: one lane per (y,z) column, 7 global loads per point -----
 // Baseline and thin-box (boundary shell) kernel.  Block = 64 (z) x 4 (y).
@@ -467,7 +384,7 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tile(const Real* __restr
 }
 
 // Resident workgroups of `kernel` on the whole device (occupancy x CUs).
-static int device_slots(const void* kernel, int block) {
+int device_slots(const void* kernel, int block) {
   int dev = 0, cus = 256, per = 1;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -480,7 +397,7 @@ static int device_slots(const void* kernel, int block) {
 // ~ rounds * (seg + 2) plane-steps per slot.  Take the cheapest segment (ties:
 // the longer one).  Measured on MI355X, 1024^3 fp64: 1 round of 511-plane
 // segments 321 GLUPS vs 8 rounds of 64 planes 313 (profiles/kernel_sweep.md).
-static int choose_segment(int64_t nx, int64_t tiles, int slots) {
+int choose_segment(int64_t nx, int64_t tiles, int slots, int halo) {
   if (nx <= 1) return 1;
   double best = 1e300;
   int pick = (int)nx;
@@ -488,7 +405,7 @@ static int choose_segment(int64_t nx, int64_t tiles, int slots) {
     const int64_t seg = (nx + parts - 1) / parts;
     const int64_t nxs = (nx + seg - 1) / seg;
     const int64_t rounds = (tiles * nxs + slots - 1) / slots;
-    const double cost = (double)rounds * (double)(seg + 2);
+    const double cost = (double)rounds * (double)(seg + halo);
     if (cost < best - 1e-9) {
       best = cost;
       pick = (int)seg;

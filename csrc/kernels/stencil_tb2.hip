@@ -1,0 +1,309 @@
+// heat3d-mi355x — 2-step temporally blocked FTCS kernel for gfx950.
+//
+// The single-step kernels are HBM-bound at 16 B/point/iteration (fp64).  This
+// kernel advances T^n -> T^{n+2} in ONE sweep: each workgroup keeps the
+// intermediate u = T^{n+1} of its tile in registers (a second x-queue next to
+// the T^n queue) and writes only T^{n+2}, i.e. 8 B read + 8 B written per point
+// per TWO iterations.  Every point still goes through the reference update
+// twice, in the same expression order and without contraction, so T^{n+2}
+// and both residuals are bitwise identical to two single-step sweeps
+// (tests/test_gpu_kernels.py).
+//
+// Tiling: overlapped tiles.  A workgroup of WZ x WY waves computes u on its
+// whole (WY*R rows) x (WZ*64*V points) tile (from T^n plus the usual 1-deep
+// halo) and T^{n+2} on the tile minus a 1-row / V-column ring; neighbouring
+// tiles overlap by that ring (2 rows, 2V columns), so each stored point is
+// produced by exactly one tile.  Boundary rows / edge points of u and T^n
+// are exchanged between the waves of a tile through LDS once per plane.
+// Points outside the update box are Dirichlet ghosts: u = T^n there.  This
+// kernel is used when the box is a whole subdomain with constant (physical)
+// ghosts on every face — the single-GPU case.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "hip_helpers.hpp"
+
+namespace heat3d {
+namespace hip {
+
+struct TB2Geom {
+  int64_t kb0;  // first u column of tile column 0 (box z0 - V)
+  int64_t yb0;  // first u row of tile row 0 (box y0 - 1)
+  int nzb, nyb, nxs, seg;
+  int64_t nblocks;
+  int xq, xr;
+};
+
+template <typename Real, int V, int R, int WZ, int WY>
+__global__ __launch_bounds__(64 * WZ * WY) void stencil_tb2(const Real* __restrict__ in,
+                                                            Real* __restrict__ out, Layout L,
+                                                            Box b, TB2Geom g, Real Dx, Real Dy,
+                                                            Real Dz, unsigned long long* res1,
+                                                            unsigned long long* res2,
+                                                            const int* done) {
+  typedef typename VecOf<Real, V>::type Vec;
+  constexpr int TZ = 64 * V;
+  constexpr int NW = WZ * WY;
+  constexpr int TZB = WZ * TZ;
+  constexpr int TYB = WY * R;
+  __shared__ Vec s_tr[2][NW][2][64];   // T^n bottom/top rows per wave
+  __shared__ Vec s_ur[2][NW][2][64];   // u bottom/top rows per wave
+  __shared__ Real s_te[2][NW][R][2];   // T^n left/right edge points per wave row
+  __shared__ Real s_ue[2][NW][R][2];   // u left/right edge points per wave row
+  if (flag_set(done)) return;
+
+  const int blk = blockIdx.x;
+  const int xcd = blk & 7;
+  int64_t t = xcd * g.xq + min(xcd, g.xr) + (blk >> 3);
+  const int zb = (int)(t % g.nzb);
+  t /= g.nzb;
+  const int ybk = (int)(t % g.nyb);
+  const int xs = (int)(t / g.nyb);
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wz = wave % WZ, wy = wave / WZ;
+  const int64_t tkb = g.kb0 + (int64_t)zb * (TZB - 2 * V);  // tile's first column
+  const int64_t tyb = g.yb0 + (int64_t)ybk * (TYB - 2);     // tile's first row
+  const int64_t kb = tkb + (int64_t)wz * TZ;
+  const int64_t k = kb + (int64_t)lane * V;
+  const int64_t yb = tyb + (int64_t)wy * R;
+  const int64_t ylo = b.lo[1], yhi = b.hi[1];
+  // rows with index <= yhi (the ghost row above the box) are loaded ("live")
+  const int rlive = (int)max((int64_t)0, min((int64_t)R, yhi + 1 - yb));
+  const int64_t xa = b.lo[0] + (int64_t)xs * g.seg;
+  const int64_t xe = min(xa + (int64_t)g.seg, b.hi[0]);
+  const int64_t sx = L.sx, sy = L.sy;
+  const int64_t xlo_live = -1, xhi_live = L.n[0];  // planes present in memory
+
+  // per-lane column predicates
+  bool zin[V];     // inside the box
+  bool zst[V];     // stored (inside box and not in the tile's V-column ring)
+  bool allst = true;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int64_t kk = k + v;
+    zin[v] = kk >= b.lo[2] && kk < b.hi[2];
+    zst[v] = zin[v] && kk >= tkb + V && kk < tkb + TZB - V;
+    allst &= zst[v];
+  }
+  const int64_t base0 = L.index(0, yb, k);
+  // outer T^n edge gather (wz == 0 left / wz == WZ-1 right)
+  const int er = lane < 32 ? lane : lane - 32;
+  const bool eload = er < rlive && yb + er >= -1 && (lane < 32 ? wz == 0 : wz == WZ - 1);
+  const int64_t ebase = L.index(0, yb + er, lane < 32 ? kb - 1 : kb + TZ);
+  const bool has_lo = wy > 0, has_hi = wy + 1 < WY;
+  const bool hb_live = !has_lo && yb - 1 >= -1 && rlive > 0;
+  const bool ht_live = !has_hi && yb + R <= yhi && rlive == R;
+
+  auto plane_live = [&](int64_t x) { return x >= xlo_live && x <= xhi_live; };
+  auto ld = [&](int64_t plane, int r) -> Vec {
+    return *reinterpret_cast<const Vec*>(in + base0 + plane * sx + (int64_t)r * sy);
+  };
+  auto load_plane = [&](int64_t x, Vec* q) {
+    const bool pl = plane_live(x);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (pl && r < rlive && yb + r >= -1) q[r] = ld(x, r);
+      else q[r] = Vec{};
+    }
+  };
+
+  Vec qm[R], qc[R], qp[R], um[R], uc[R];
+  load_plane(xa - 2, qm);
+  load_plane(xa - 1, qc);
+  load_plane(xa, qp);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    um[r] = Vec{};
+    uc[r] = Vec{};
+  }
+  Vec hb = {}, ht = {};
+  Real ed = Real(0);
+  if (plane_live(xa - 1)) {
+    if (hb_live) hb = ld(xa - 1, -1);
+    if (ht_live) ht = ld(xa - 1, R);
+    if (eload) ed = in[ebase + (xa - 1) * sx];
+  }
+
+  double m1 = 0.0, m2 = 0.0;
+  int par = 0;
+  for (int64_t x = xa - 1; x <= xe; ++x) {
+    // publish T^n(x) and u(x-1) boundary rows / edge points
+    s_tr[par][wave][0][lane] = qc[0];
+    s_tr[par][wave][1][lane] = qc[R - 1];
+    s_ur[par][wave][0][lane] = uc[0];
+    s_ur[par][wave][1][lane] = uc[R - 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (lane == 0) {
+        s_te[par][wave][r][0] = qc[r][0];
+        s_ue[par][wave][r][0] = uc[r][0];
+      }
+      if (lane == 63) {
+        s_te[par][wave][r][1] = qc[r][V - 1];
+        s_ue[par][wave][r][1] = uc[r][V - 1];
+      }
+    }
+    // prefetch T^n(x+2) and the outer halo of plane x+1
+    Vec qn[R];
+    load_plane(x + 2, qn);
+    Vec hbn = {}, htn = {};
+    Real edn = Real(0);
+    if (plane_live(x + 1)) {
+      if (hb_live) hbn = ld(x + 1, -1);
+      if (ht_live) htn = ld(x + 1, R);
+      if (eload) edn = in[ebase + (x + 1) * sx];
+    }
+    __syncthreads();
+
+    // ---- u(x) = FTCS(T^n) inside the box, T^n outside (Dirichlet ghosts)
+    const bool xin = x >= b.lo[0] && x < b.hi[0];
+    Vec un[R];
+    {
+      const Vec tlo = has_lo ? s_tr[par][wave - WZ][1][lane] : hb;
+      const Vec thi = has_hi ? s_tr[par][wave + WZ][0][lane] : ht;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const Vec c = qc[r];
+        const Vec ym = r == 0 ? tlo : qc[r > 0 ? r - 1 : 0];
+        const Vec yp = r == R - 1 ? thi : qc[r + 1 < R ? r + 1 : 0];
+        const Real left = wz > 0 ? s_te[par][wave - 1][r][1] : readlane(ed, r);
+        const Real right = wz + 1 < WZ ? s_te[par][wave + 1][r][0] : readlane(ed, 32 + r);
+        const bool yin = xin && (yb + r >= ylo) && (yb + r < yhi);
+        Vec u;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const Real zm = v == 0 ? dpp_shr1(left, c[V - 1]) : c[v > 0 ? v - 1 : 0];
+          const Real zp = v == V - 1 ? dpp_shl1(right, c[0]) : c[v + 1 < V ? v + 1 : 0];
+          const Real nv = ftcs<Real>(c[v], qm[r][v], qp[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
+          const bool in_box = yin && zin[v];
+          u[v] = in_box ? nv : c[v];
+          if (in_box) m1 = res_max(m1, fabs((double)nv - (double)c[v]));
+        }
+        un[r] = u;
+      }
+    }
+
+    // ---- T^{n+2}(x-1) = FTCS(u) on the stored region
+    const int64_t xo = x - 1;
+    if (xo >= xa && xo < xe) {
+      const Vec ulo = has_lo ? s_ur[par][wave - WZ][1][lane] : uc[0];
+      const Vec uhi = has_hi ? s_ur[par][wave + WZ][0][lane] : uc[R - 1];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int64_t row = yb + r;
+        // stored rows: inside the box and not in the tile's 1-row ring
+        const bool rst = row >= ylo && row < yhi && row >= tyb + 1 && row < tyb + TYB - 1;
+        const Vec c = uc[r];
+        const Vec ym = r == 0 ? ulo : uc[r > 0 ? r - 1 : 0];
+        const Vec yp = r == R - 1 ? uhi : uc[r + 1 < R ? r + 1 : 0];
+        const Real left = wz > 0 ? s_ue[par][wave - 1][r][1] : c[0];
+        const Real right = wz + 1 < WZ ? s_ue[par][wave + 1][r][0] : c[V - 1];
+        Vec nv;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const Real zm = v == 0 ? dpp_shr1(left, c[V - 1]) : c[v > 0 ? v - 1 : 0];
+          const Real zp = v == V - 1 ? dpp_shl1(right, c[0]) : c[v + 1 < V ? v + 1 : 0];
+          nv[v] = ftcs<Real>(c[v], um[r][v], un[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
+          if (rst && zst[v]) m2 = res_max(m2, fabs((double)nv[v] - (double)c[v]));
+        }
+        if (rst) {
+          Real* dst = out + base0 + xo * sx + (int64_t)r * sy;
+          if (allst) {
+            *reinterpret_cast<Vec*>(dst) = nv;
+          } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+              if (zst[v]) dst[v] = nv[v];
+          }
+        }
+      }
+    }
+    // ---- rotate queues
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      qm[r] = qc[r];
+      qc[r] = qp[r];
+      qp[r] = qn[r];
+      um[r] = uc[r];
+      uc[r] = un[r];
+    }
+    hb = hbn;
+    ht = htn;
+    ed = edn;
+    par ^= 1;
+  }
+  if (res1) residual_commit(res1, m1);
+  if (res2) residual_commit(res2, m2);
+}
+
+template <typename Real, int V, int R, int WZ, int WY>
+static void launch_tb2(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
+  const Box& b = p.box;
+  constexpr int TZ = 64 * V;
+  constexpr int TZB = WZ * TZ, TYB = WY * R;
+  static_assert(TYB > 2 && TZB > 2 * V, "tile too small");
+  TB2Geom g;
+  g.kb0 = ((b.lo[2] - V) / V) * V;
+  if (g.kb0 > b.lo[2] - V) g.kb0 -= V;  // floor for negative values
+  g.yb0 = b.lo[1] - 1;
+  // tiles step by (TZB - 2V) columns and (TYB - 2) rows; stored columns of
+  // tile zb: [kb0 + zb*(TZB-2V) + V, ... + TZB - V)
+  const int64_t zspan = b.hi[2] - (g.kb0 + V);
+  g.nzb = (int)std::max<int64_t>(1, (zspan + (TZB - 2 * V) - 1) / (TZB - 2 * V));
+  const int64_t yspan = b.hi[1] - (g.yb0 + 1);
+  g.nyb = (int)std::max<int64_t>(1, (yspan + (TYB - 2) - 1) / (TYB - 2));
+  int seg = k.L;
+  if (seg <= 0) {
+    static int slots = 0;
+    if (!slots) slots = device_slots(reinterpret_cast<const void*>(&stencil_tb2<Real, V, R, WZ, WY>),
+                                     64 * WZ * WY);
+    seg = choose_segment(b.extent(0), (int64_t)g.nzb * g.nyb, slots, 4);
+  }
+  g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));
+  g.nxs = (int)((b.extent(0) + g.seg - 1) / g.seg);
+  g.nblocks = (int64_t)g.nzb * g.nyb * g.nxs;
+  HEAT3D_CHECK(g.nblocks < (1LL << 31), "too many blocks");
+  g.xq = (int)(g.nblocks / 8);
+  g.xr = (int)(g.nblocks % 8);
+  unsigned long long* r1 = p.state ? &p.state->residual[p.slot] : nullptr;
+  unsigned long long* r2 = p.state ? &p.state->residual[p.slot ^ 1] : nullptr;
+  const int* done = p.state ? &p.state->done : nullptr;
+  hipLaunchKernelGGL((stencil_tb2<Real, V, R, WZ, WY>), dim3((unsigned)g.nblocks),
+                     dim3(64 * WZ * WY), 0, s, static_cast<const Real*>(p.in),
+                     static_cast<Real*>(p.out), p.L, b, g, (Real)p.D[0], (Real)p.D[1],
+                     (Real)p.D[2], r1, r2, done);
+  HIPK_CHECK(hipGetLastError());
+}
+
+template <typename Real>
+static void dispatch_tb2(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
+  const int V = k.V ? k.V : (sizeof(Real) == 8 ? 2 : 4);
+  const int R = k.R ? k.R : 4;
+  const int WZ = k.WZ ? k.WZ : 2, WY = k.WY ? k.WY : 4;
+#define H3D_TB2(VV, RR, ZZ, YY)                      \
+  if (V == VV && R == RR && WZ == ZZ && WY == YY) {  \
+    launch_tb2<Real, VV, RR, ZZ, YY>(p, k, s);       \
+    return;                                          \
+  }
+  H3D_TB2(2, 4, 2, 4) H3D_TB2(2, 4, 4, 2) H3D_TB2(2, 4, 1, 4) H3D_TB2(2, 4, 2, 2)
+  H3D_TB2(2, 8, 2, 2) H3D_TB2(2, 8, 4, 1) H3D_TB2(2, 6, 2, 2) H3D_TB2(2, 4, 4, 4)
+  H3D_TB2(2, 2, 2, 8)
+  if constexpr (sizeof(Real) == 4) {
+    H3D_TB2(4, 4, 2, 4) H3D_TB2(4, 4, 2, 2) H3D_TB2(4, 8, 2, 2) H3D_TB2(4, 4, 1, 4)
+  }
+#undef H3D_TB2
+  HEAT3D_THROW("unsupported tb2 kernel variant V=" << V << " R=" << R << " WZ=" << WZ
+               << " WY=" << WY);
+}
+
+void stencil2(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
+  if (p.box.empty()) return;
+  if (t == DType::F64) dispatch_tb2<double>(p, k, S(stream));
+  else dispatch_tb2<float>(p, k, S(stream));
+}
+
+}  // namespace hip
+}  // namespace heat3d

@@ -231,6 +231,16 @@ PYBIND11_MODULE(_heat3d, m) {
     auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
     hip::stencil(t, p, KernelSpec::parse(kernel), reinterpret_cast<void*>(stream));
   });
+  hk.def("stencil2", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
+                        std::array<double, 3> D, int64_t state_ptr, int slot, const std::string& kernel,
+                        int64_t stream) {
+    DType t = dt_of(dt);
+    std::array<int64_t, 6> box = {0, n[0], 0, n[1], 0, n[2]};
+    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
+    KernelSpec k = KernelSpec::parse(kernel);
+    k.kind = KernelSpec::TB2;
+    hip::stencil2(t, p, k, reinterpret_cast<void*>(stream));
+  });
   hk.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
                           std::array<int64_t, 3> N, std::array<double, 3> h, int64_t stream) {
     DType t = dt_of(dt);
@@ -384,6 +394,7 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("interior_points", &Solver::interior_points)
       .def_property_readonly("iterations_issued", &Solver::iterations_issued)
       .def_property_readonly("kernel_name", &Solver::kernel_name)
+      .def_property_readonly("temporal_blocking", &Solver::temporal_blocking)
       .def_property_readonly("backend_name", [](Solver& s) { return std::string(s.backend().name()); })
       .def_property_readonly("comm_name", [](Solver& s) { return std::string(s.comm().name()); })
       .def_property_readonly("comm_size", [](Solver& s) { return s.comm().size(); })

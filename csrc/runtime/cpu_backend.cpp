@@ -50,6 +50,25 @@ class CpuBackend final : public Backend {
   void stencil(DType t, const StencilParams& p, const KernelSpec&, StreamId) override {
     cpu::stencil(t, p);
   }
+  // Reference semantics of the 2-step kernel: two single steps through a
+  // scratch field (same ghosts), residual slots slot and slot^1.
+  void stencil2(DType t, const StencilParams& p, const KernelSpec&, StreamId) override {
+    if (p.state && p.state->done) return;
+    if (scratch_bytes_ < p.L.bytes()) {
+      release(scratch_);
+      scratch_ = alloc(p.L.bytes());
+      scratch_bytes_ = p.L.bytes();
+    }
+    std::memcpy(scratch_, p.in, p.L.bytes());
+    StencilParams a = p;
+    a.out = scratch_;
+    cpu::stencil(t, a);
+    StencilParams b = p;
+    b.in = scratch_;
+    b.slot = p.slot ^ 1;
+    cpu::stencil(t, b);
+  }
+  ~CpuBackend() override { release(scratch_); }
   void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, StreamId) override {
     cpu::pack_box(t, f, L, b, buf);
   }
@@ -71,6 +90,12 @@ class CpuBackend final : public Backend {
             StreamId) override {
     cpu::poke(t, f, L, i, j, k, value);
   }
+
+ private:
+  void* scratch_ = nullptr;
+  std::size_t scratch_bytes_ = 0;
+
+ public:
   void box_bitsum(DType t, const void* f, const Layout& L, const Box& b, unsigned long long* out,
                   StreamId) override {
     *out = cpu::box_bitsum(t, f, L, b);

@@ -158,6 +158,9 @@ class HipBackend final : public Backend {
   void stencil(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) override {
     hip::stencil(t, p, k, streams_[s]);
   }
+  void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) override {
+    hip::stencil2(t, p, k, streams_[s]);
+  }
   void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, StreamId s) override {
     hip::pack_box(t, f, L, b, buf, streams_[s]);
   }

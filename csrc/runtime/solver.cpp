@@ -34,8 +34,8 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     if (parts.size() > 3) k.L = std::atoi(parts[3].c_str());
     if (parts.size() > 4) k.O = std::atoi(parts[4].c_str());
     if (parts.size() > 5) k.NT = std::atoi(parts[5].c_str());
-  } else if (parts[0] == "tile") {
-    k.kind = Tile;
+  } else if (parts[0] == "tile" || parts[0] == "tb2") {
+    k.kind = parts[0] == "tile" ? Tile : TB2;
     auto at = [&](std::size_t i) { return parts.size() > i ? std::atoi(parts[i].c_str()) : 0; };
     k.V = at(1);
     k.R = at(2);
@@ -52,9 +52,10 @@ KernelSpec KernelSpec::parse(const std::string& s) {
 
 std::string KernelSpec::str() const {
   if (kind == Naive) return "naive";
-  if (kind == Tile) {
+  if (kind == Tile || kind == TB2) {
     std::ostringstream os;
-    os << "tile:" << V << ":" << R << ":" << WZ << ":" << WY << ":" << L << ":" << NT;
+    os << (kind == Tile ? "tile:" : "tb2:") << V << ":" << R << ":" << WZ << ":" << WY << ":" << L
+       << ":" << NT;
     return os.str();
   }
   std::ostringstream os;
@@ -78,8 +79,10 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
                                << comm_->size() << " ranks");
   dec_ = Decomposition::make(cfg_.n, dims);
   kspec_ = KernelSpec::parse(cfg_.kernel);
+  if (kspec_.kind == KernelSpec::TB2) kspec_.kind = KernelSpec::Tile;
+  kspec2_ = KernelSpec::parse(cfg_.kernel2);
+  kspec2_.kind = KernelSpec::TB2;
   overlap_ = cfg_.overlap;
-  if (comm_->all_local() && !be_->is_gpu()) overlap_ = cfg_.overlap;
 
   for (int r : comm_->local_ranks()) {
     Local l;
@@ -94,6 +97,10 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     local_.push_back(l);
   }
   setup_faces();
+  // 2-step temporal blocking: one halo-free subdomain (its ghosts are all
+  // Dirichlet), on by default on the GPU, opt-in on the CPU backend (tests)
+  tb2_ = local_.size() == 1 && !has_halo_ && kspec_.kind != KernelSpec::Naive &&
+         (cfg_.temporal == 2 || (cfg_.temporal == 0 && be_->is_gpu()));
   dstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
   hstate_ = static_cast<DeviceState*>(be_->alloc_host(2 * sizeof(DeviceState)));
   std::memset(hstate_, 0, 2 * sizeof(DeviceState));
@@ -225,6 +232,9 @@ void Solver::initialize() {
   be_->copy(dstate_, hstate_, sizeof(DeviceState), CopyKind::H2D, kCompute);
   be_->sync(kCompute);
   issued_ = 0;
+  phase_ = 0;
+  segs_.clear();
+  seg_head_ = 0;
   if (!cfg_.restart.empty()) load_checkpoint(cfg_.restart);
   // make every pipeline event valid (complete) before the first iteration
   for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
@@ -238,8 +248,8 @@ void Solver::initialize() {
 }
 
 // --- one iteration -----------------------------------------------------------
-void Solver::enqueue_halo(int p) {
-  const StreamId s = overlap_ ? kComm : kCompute;
+void Solver::enqueue_halo(int p, StreamId s) {
+  // p = buffer index whose faces / ghosts are exchanged
   be_->range_push("halo");
   if (comm_->all_local()) {
     for (auto& l : local_)
@@ -295,12 +305,13 @@ static bool trace_on() {
     }                                                                    \
   } while (0)
 
-void Solver::enqueue_iteration(int p) {
-  H3D_TRACE("iteration issued=" << issued_ << " parity=" << p << (capturing_ ? " (capturing)" : ""));
+void Solver::enqueue_iteration(int p, int bi) {
+  H3D_TRACE("iteration issued=" << issued_ << " parity=" << p << " buf=" << bi
+                                << (capturing_ ? " (capturing)" : ""));
   auto params = [&](Local& l, const Box& b) {
     StencilParams sp;
-    sp.in = l.field[p];
-    sp.out = l.field[p ^ 1];
+    sp.in = l.field[bi];
+    sp.out = l.field[bi ^ 1];
     sp.L = l.L;
     sp.box = b;
     for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
@@ -326,7 +337,7 @@ void Solver::enqueue_iteration(int p) {
     ev_wait(kComm, EV_INT + (p ^ 1));  // interior of t-1 done (RAW on layer 1, WAR on shell)
     ev_wait(kComm, EV_CHK + p);
     T(2, kComm);
-    enqueue_halo(p);
+    enqueue_halo(bi, kComm);
     T(3, kComm);
     be_->range_push("shell");
     for (auto& l : local_)
@@ -336,7 +347,7 @@ void Solver::enqueue_iteration(int p) {
     ev_record(EV_BND + p, kComm);
   } else {
     T(2, kCompute);
-    if (has_halo_) enqueue_halo(p);
+    if (has_halo_) enqueue_halo(bi, kCompute);
     T(3, kCompute);
     be_->range_push("sweep");
     for (auto& l : local_) be_->stencil(dt_, params(l, l.owned), kspec_, kCompute);
@@ -356,6 +367,71 @@ void Solver::enqueue_iteration(int p) {
   ev_record(EV_CHK + p, kReduce);
 }
 
+// Two iterations t, t+1 (slots p, p^1) as one temporally blocked sweep of the
+// single subdomain: T^t in field[bi] -> T^{t+2} in field[bi^1], both residuals
+// fused, then both convergence checks, all on the compute stream.  The next
+// pair is queued behind those checks, so once converged it is a no-op and
+// field[bi] (T^t) stays intact for the rollback in finalize_converged().
+void Solver::enqueue_double(int p, int bi) {
+  H3D_TRACE("double issued=" << issued_ << " parity=" << p << " buf=" << bi
+                             << (capturing_ ? " (capturing)" : ""));
+  HEAT3D_CHECK(local_.size() == 1 && !has_halo_, "temporal blocking needs one halo-free subdomain");
+  Local& l = local_[0];
+  ev_wait(kCompute, EV_CHK + 0);
+  ev_wait(kCompute, EV_CHK + 1);
+  StencilParams sp;
+  sp.in = l.field[bi];
+  sp.out = l.field[bi ^ 1];
+  sp.L = l.L;
+  sp.box = l.owned;
+  for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+  sp.state = dstate_;
+  sp.slot = p;
+  be_->range_push("sweep2");
+  be_->stencil2(dt_, sp, kspec2_, kCompute);
+  be_->range_pop();
+  be_->check_convergence(dstate_, p, kCompute);
+  be_->check_convergence(dstate_, p ^ 1, kCompute);
+  ev_record(EV_INT + 0, kCompute);
+  ev_record(EV_INT + 1, kCompute);
+  ev_record(EV_CHK + 0, kCompute);
+  ev_record(EV_CHK + 1, kCompute);
+}
+
+void Solver::record_segment(int64_t start, int len, int inbuf) {
+  const std::size_t cap = 1 << 14;
+  if (segs_.size() < cap) segs_.push_back({start, len, inbuf});
+  else segs_[seg_head_ % cap] = {start, len, inbuf};
+  ++seg_head_;
+}
+
+// After convergence at iteration c the final field is T^{c+1}.  Find the
+// segment that computed iteration c; a temporally blocked pair that met the
+// criterion in its first half stored T^{c+2}, so recompute T^{c+1} from its
+// (untouched) input buffer with one forced single step.
+void Solver::finalize_converged(int64_t c) {
+  be_->sync_all();
+  const Segment* hit = nullptr;
+  for (const auto& s : segs_)
+    if (c >= s.start && c < s.start + s.len) hit = &s;
+  HEAT3D_CHECK(hit, "segment of converged iteration " << c << " not recorded");
+  const Segment s = *hit;
+  if (s.len == 2 && c == s.start) {
+    Local& l = local_[0];
+    StencilParams sp;
+    sp.in = l.field[s.inbuf];
+    sp.out = l.field[s.inbuf ^ 1];
+    sp.L = l.L;
+    sp.box = l.owned;
+    for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+    sp.state = nullptr;  // forced: ignores the done flag, no residual
+    be_->stencil(dt_, sp, kspec_, kCompute);
+    be_->sync(kCompute);
+  }
+  issued_ = c + 1;
+  phase_ = (int)(((s.inbuf ^ 1) - (c + 1)) & 1);
+}
+
 void Solver::accumulate_phase_times() {
   be_->sync_all();
   static const char* names[] = {"interior_ms", "halo_ms", "shell_ms", "reduce_check_ms", "iteration_ms"};
@@ -370,8 +446,13 @@ void Solver::accumulate_phase_times() {
 
 void Solver::build_graph() {
   H3D_TRACE("build_graph at issued=" << issued_);
-  const int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
+  // G iterations per graph; temporally blocked graphs hold an even number of
+  // pairs so that the buffer roles repeat (G multiple of 4)
+  int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
+  if (tb2_) G = std::max(4, G - (G % 4));
+  graph_kind_ = tb2_ ? 2 : 1;
   graph_parity_ = (int)(issued_ & 1);
+  graph_buf_ = cur();
   bool saved[EV_COUNT];
   std::memcpy(saved, ev_valid_, sizeof(saved));
   Event saved_cur[EV_COUNT];
@@ -386,7 +467,11 @@ void Solver::build_graph() {
     ev_record(EV_FORK, kCompute);
     ev_wait(kComm, EV_FORK);
     ev_wait(kReduce, EV_FORK);
-    for (int i = 0; i < G; ++i) enqueue_iteration((graph_parity_ + i) & 1);
+    if (graph_kind_ == 2) {
+      for (int i = 0; i < G / 2; ++i) enqueue_double(graph_parity_, (graph_buf_ + i) & 1);
+    } else {
+      for (int i = 0; i < G; ++i) enqueue_iteration((graph_parity_ + i) & 1, (graph_buf_ + i) & 1);
+    }
     ev_record(EV_JCOMM, kComm);
     ev_record(EV_JRED, kReduce);
     ev_wait(kCompute, EV_JCOMM);
@@ -424,14 +509,33 @@ void Solver::run_chunk(int64_t n) {
   }();
   const bool graphs = cfg_.use_graph && be_->supports_graphs() && comm_->capturable() &&
                       !graph_failed_ && !phase_timing_ && (!overlap_ || ms_ok);
+  const int want_kind = tb2_ ? 2 : 1;
   while (n > 0) {
-    const int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
-    if (graphs && n >= G && (graph_ == nullptr || (int)(issued_ & 1) == graph_parity_)) {
+    int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
+    if (tb2_) G = std::max(4, G - (G % 4));
+    if (graph_ && graph_kind_ != want_kind) {
+      be_->sync_all();
+      be_->destroy_graph(graph_);
+      graph_ = nullptr;
+    }
+    const bool aligned = graph_ && (int)(issued_ & 1) == graph_parity_ && cur() == graph_buf_;
+    if (graphs && n >= G && (graph_ == nullptr || aligned)) {
       if (!graph_) build_graph();
-      if (graph_ && (int)(issued_ & 1) == graph_parity_) {
+      if (graph_ && (int)(issued_ & 1) == graph_parity_ && cur() == graph_buf_) {
         H3D_TRACE("launch_graph issued=" << issued_);
         be_->launch_graph(graph_);
-        issued_ += graph_iters_;
+        if (graph_kind_ == 2) {
+          for (int i = 0; i < graph_iters_ / 2; ++i) {
+            record_segment(issued_, 2, cur());
+            issued_ += 2;
+            phase_ ^= 1;
+          }
+        } else {
+          for (int i = 0; i < graph_iters_; ++i) {
+            record_segment(issued_, 1, cur());
+            ++issued_;
+          }
+        }
         n -= graph_iters_;
         // the graph joined every stream into compute: re-fork for eager work
         for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
@@ -441,9 +545,18 @@ void Solver::run_chunk(int64_t n) {
         continue;
       }
     }
+    if (tb2_ && n >= 2 && !phase_timing_) {
+      record_segment(issued_, 2, cur());
+      enqueue_double((int)(issued_ & 1), cur());
+      issued_ += 2;
+      phase_ ^= 1;
+      n -= 2;
+      continue;
+    }
     if (phase_timing_ && !tev_[0])
       for (auto& e : tev_) e = be_->event_create();
-    enqueue_iteration((int)(issued_ & 1));
+    record_segment(issued_, 1, cur());
+    enqueue_iteration((int)(issued_ & 1), cur());
     if (phase_timing_) accumulate_phase_times();
     ++issued_;
     --n;
@@ -553,14 +666,14 @@ RunResult Solver::run() {
   R.norm = hs.norm;
   R.last_residual = hs.last_residual;
   // the final field is T^{iterations}: point the "current" parity at it
-  if (hs.done) issued_ = R.iterations;
+  if (hs.done) finalize_converged(hs.conv_iter);
   R.glups = R.seconds > 0 ? (double)interior_points() * (double)R.issued / R.seconds / 1e9 : 0.0;
   return R;
 }
 
 void Solver::compute_error(double* global_mean, double* local_mean) {
   be_->sync_all();
-  const int p = (int)(issued_ & 1);
+  const int p = cur();
   const std::size_t off = offsetof(DeviceState, error_sum);
   char* base = reinterpret_cast<char*>(dstate_);
   be_->memset(base + off, 0, 2 * sizeof(double), kCompute);
@@ -594,7 +707,7 @@ std::vector<double> Solver::local_field(int idx, bool with_ghosts) {
   }
   const std::size_t bytes = b.volume() * esize_;
   void* dbuf = be_->alloc(bytes);
-  be_->pack_box(dt_, l.field[issued_ & 1], l.L, b, dbuf, kCompute);
+  be_->pack_box(dt_, l.field[cur()], l.L, b, dbuf, kCompute);
   std::vector<char> h(bytes);
   be_->copy(h.data(), dbuf, bytes, CopyKind::D2H, kCompute);
   be_->sync(kCompute);
@@ -610,7 +723,7 @@ bool Solver::gather_global(std::vector<double>* out) {
   be_->sync_all();
   const int P = comm_->size();
   const bool root = is_root();
-  const int p = (int)(issued_ & 1);
+  const int p = cur();
   const int64_t* N = dec_.N;
   if (root) out->assign((std::size_t)(N[0] * N[1] * N[2]), 0.0);
   int64_t maxvol = 0;
@@ -710,7 +823,7 @@ void Solver::save_checkpoint(const std::string& dir) {
   HostState hs = state();
   io::make_dirs(dir);
   const std::string raw = dir + "/field.raw";
-  const int p = (int)(issued_ & 1);
+  const int p = cur();
   const int64_t* N = dec_.N;
   {
     int fd = io::open_raw(raw, true);
@@ -798,6 +911,7 @@ void Solver::load_checkpoint(const std::string& dir) {
   be_->copy(dstate_, hstate_, sizeof(DeviceState), CopyKind::H2D, kCompute);
   be_->sync(kCompute);
   issued_ = it;
+  phase_ = 0;
 }
 
 int Solver::verify_halos() {
@@ -805,7 +919,7 @@ int Solver::verify_halos() {
   if (issued_ == 0 || !has_halo_) return 0;
   // input buffer of the last iteration: its ghosts were filled by that
   // iteration's exchange from the neighbours' (unchanged) faces
-  const int p = (int)((issued_ - 1) & 1);
+  const int p = cur() ^ 1;  // single-step schedule (halos imply no temporal blocking)
   int nf = 0;
   for (auto& l : local_) nf += (int)l.faces.size();
   auto* dsum = static_cast<unsigned long long*>(be_->alloc(sizeof(unsigned long long) * 3 * nf));
@@ -883,7 +997,7 @@ void Solver::inject(int idx, int64_t i, int64_t j, int64_t k, double value, bool
   auto& l = local_.at(idx);
   HEAT3D_CHECK(i >= -1 && i <= l.sd.n[0] && j >= -1 && j <= l.sd.n[1] && k >= -1 && k <= l.sd.n[2],
                "inject index outside the ghosted block");
-  be_->poke(dt_, l.field[(issued_ + (previous ? 1 : 0)) & 1], l.L, i, j, k, value, kCompute);
+  be_->poke(dt_, l.field[cur() ^ (previous ? 1 : 0)], l.L, i, j, k, value, kCompute);
   be_->sync(kCompute);
 }
 

@@ -95,7 +95,9 @@ class Solver {
   const Subdomain& local_subdomain(int i) const { return local_[i].sd; }
   const Layout& local_layout(int i) const { return local_[i].L; }
   // current field buffer of a local subdomain (device pointer on HIP)
-  void* local_field_ptr(int i) { return local_[i].field[issued_ & 1]; }
+  void* local_field_ptr(int i) { return local_[i].field[cur()]; }
+  // True when iterations run as 2-step temporally blocked sweeps.
+  bool temporal_blocking() const { return tb2_; }
 
   // Output / checkpoint.
   void write_tecplot(const std::string& path, const std::string& layout);
@@ -141,8 +143,15 @@ class Solver {
   };
 
   void setup_faces();
-  void enqueue_iteration(int p);
-  void enqueue_halo(int p);
+  // one single-step iteration: residual slot / event parity p, input buffer bi
+  void enqueue_iteration(int p, int bi);
+  // two iterations in one temporally blocked sweep (single stream)
+  void enqueue_double(int p, int bi);
+  void enqueue_halo(int bi, StreamId s);
+  // buffer holding T^{issued_}
+  int cur() const { return (int)((issued_ + phase_) & 1); }
+  void record_segment(int64_t start, int len, int inbuf);
+  void finalize_converged(int64_t conv_iter);
   void poll_enqueue(StreamId s);
   void ev_record(int id, StreamId s);
   void ev_wait(StreamId s, int id);
@@ -165,6 +174,17 @@ class Solver {
   DeviceState* dstate_ = nullptr;   // device
   DeviceState* hstate_ = nullptr;   // pinned host mirror
   int64_t issued_ = 0;              // iterations enqueued so far (absolute index)
+  // T^t lives in field[(t + phase_) & 1]; a 2-step sweep flips phase_
+  int phase_ = 0;
+  bool tb2_ = false;
+  KernelSpec kspec2_;
+  struct Segment {
+    int64_t start;
+    int len;    // 1 = single step, 2 = temporally blocked pair
+    int inbuf;  // buffer read by the segment
+  };
+  std::vector<Segment> segs_;       // ring of recent segments (for convergence rollback)
+  std::size_t seg_head_ = 0;
 
   // events: 0..1 int[p], 2..3 bnd[p], 4..5 check[p], 6 fork, 7 join comm, 8 join red, 9..10 poll
   enum { EV_INT = 0, EV_BND = 2, EV_CHK = 4, EV_FORK = 6, EV_JCOMM = 7, EV_JRED = 8, EV_POLL = 9,
@@ -179,6 +199,8 @@ class Solver {
   void* graph_ = nullptr;
   int graph_iters_ = 0;
   int graph_parity_ = 0;
+  int graph_buf_ = 0;     // input buffer at the start of the captured chunk
+  int graph_kind_ = 1;    // 1 = single-step iterations, 2 = temporally blocked pairs
   bool graph_failed_ = false;
 
   bool phase_timing_ = false;
