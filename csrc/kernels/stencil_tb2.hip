@@ -280,19 +280,24 @@ static void launch_tb2(const StencilParams& p, const KernelSpec& k, hipStream_t 
 
 template <typename Real>
 static void dispatch_tb2(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
-  const int V = k.V ? k.V : (sizeof(Real) == 8 ? 2 : 4);
-  const int R = k.R ? k.R : 4;
-  const int WZ = k.WZ ? k.WZ : 2, WY = k.WY ? k.WY : 4;
+  // defaults from the MI355X sweep (profiles/kernel_sweep.md): one wave per
+  // tile column, 8 (fp64) / 4 (fp32) waves stacked in y
+  const bool f64 = sizeof(Real) == 8;
+  const int V = k.V ? k.V : (f64 ? 2 : 4);
+  const int R = k.R ? k.R : (f64 ? 4 : 3);
+  const int WZ = k.WZ ? k.WZ : 1, WY = k.WY ? k.WY : (f64 ? 8 : 4);
 #define H3D_TB2(VV, RR, ZZ, YY)                      \
   if (V == VV && R == RR && WZ == ZZ && WY == YY) {  \
     launch_tb2<Real, VV, RR, ZZ, YY>(p, k, s);       \
     return;                                          \
   }
   H3D_TB2(2, 4, 2, 4) H3D_TB2(2, 4, 4, 2) H3D_TB2(2, 4, 1, 4) H3D_TB2(2, 4, 2, 2)
-  H3D_TB2(2, 8, 2, 2) H3D_TB2(2, 8, 4, 1) H3D_TB2(2, 6, 2, 2) H3D_TB2(2, 4, 4, 4)
-  H3D_TB2(2, 2, 2, 8)
+  H3D_TB2(2, 8, 2, 2) H3D_TB2(2, 6, 2, 2) H3D_TB2(2, 2, 2, 8)
+  H3D_TB2(2, 4, 1, 2) H3D_TB2(2, 4, 1, 8) H3D_TB2(2, 6, 1, 4) H3D_TB2(2, 8, 1, 4)
+  H3D_TB2(2, 2, 1, 8) H3D_TB2(2, 3, 1, 4) H3D_TB2(2, 5, 1, 4) H3D_TB2(2, 6, 1, 2)
   if constexpr (sizeof(Real) == 4) {
-    H3D_TB2(4, 4, 2, 4) H3D_TB2(4, 4, 2, 2) H3D_TB2(4, 8, 2, 2) H3D_TB2(4, 4, 1, 4)
+    H3D_TB2(4, 4, 2, 4) H3D_TB2(4, 4, 2, 2) H3D_TB2(4, 4, 1, 4) H3D_TB2(4, 4, 1, 8)
+    H3D_TB2(4, 2, 1, 8) H3D_TB2(4, 6, 1, 4) H3D_TB2(4, 4, 1, 2) H3D_TB2(4, 3, 1, 4)
   }
 #undef H3D_TB2
   HEAT3D_THROW("unsupported tb2 kernel variant V=" << V << " R=" << R << " WZ=" << WZ

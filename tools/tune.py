@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--probes", action="store_true", help="also run the HBM copy/read probes")
     a = ap.parse_args()
 
     import torch
@@ -48,7 +49,7 @@ def main():
     esize = 8 if a.dtype == "fp64" else 4
     res = {v: [] for v in a.variants}
     for v in a.variants:  # warm / compile / validate
-        ops.ftcs_step(f0, f1, D, kernel=v, state=state)
+        (ops.ftcs_step2 if v.startswith('tb2') else ops.ftcs_step)(f0, f1, D, kernel=v, state=state)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(a.rounds):
@@ -56,18 +57,18 @@ def main():
             e0.record()
             for i in range(a.iters):
                 src, dst = (f0, f1) if i % 2 == 0 else (f1, f0)
-                ops.ftcs_step(src, dst, D, kernel=v, state=state)
+                (ops.ftcs_step2 if v.startswith('tb2') else ops.ftcs_step)(src, dst, D, kernel=v, state=state)
             e1.record()
             e1.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
-            res[v].append(pts / (ms * 1e-3) / 1e9)
+            res[v].append((2 if v.startswith('tb2') else 1) * pts / (ms * 1e-3) / 1e9)
     # HBM calibration on the same buffers: 16 B/lane copy and read-only sweeps
     ext = heat3d_amd.native()
     nbytes = (f0.flat.numel() * esize) // 4096 * 4096
     strm = torch.cuda.current_stream().cuda_stream
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
     probes = ((0, "copy"), (1, "read"), (2, "copy_x4"), (3, "copy_x4_nt"), (4, "copy_chunk"))
-    for blocks in (1024, 2048, 8192):
+    for blocks in ((1024, 2048, 8192) if a.probes else ()):
         for kind, name in probes:
             ts = []
             for _ in range(a.rounds):
