@@ -42,6 +42,9 @@ def main() -> int:
     ap.add_argument("--graph-chunk", type=int, default=32)
     ap.add_argument("--converge-eps", type=float, default=1e-3,
                     help="also measure time-to-converge at this EPS (0 disables)")
+    ap.add_argument("--temporal", type=int, default=0, help="0 auto | 1 single-step | 2 two-step pairs")
+    ap.add_argument("--virtual-ranks", type=int, default=1,
+                    help="diagnostic: split the grid into this many subdomains on one GPU (not the headline)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -74,13 +77,17 @@ def main() -> int:
         dims = best_dims_for(N, world, None if args.decomp == "auto" else args.decomp)
     else:
         dims = tuple(int(v) for v in args.decomp.lower().split("x"))
-    assert dims[0] * dims[1] * dims[2] == world
+    if args.virtual_ranks > 1:
+        assert world == 1, "--virtual-ranks is a single-process diagnostic"
+        dims = best_dims_for(N, args.virtual_ranks, None if args.decomp == "auto" else args.decomp)
+    assert dims[0] * dims[1] * dims[2] == world * args.virtual_ranks
 
     def make(eps, iter_max):
         return HeatSolver(N, iter_max=iter_max, eps=eps, dtype=args.dtype, backend="hip",
                           decomp=dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
-                          device=dev, group=group)
+                          device=dev, group=group, virtual_ranks=args.virtual_ranks,
+                          extra_args=["--temporal", str(args.temporal)])
 
     s = make(0.0, 1 << 40)
     s.initialize()
@@ -130,7 +137,8 @@ def main() -> int:
         "dtype": args.dtype,
         "data": "synthetic (analytic Dirichlet IC/BC of the reference, random-free)",
         "config": {"model": f"heat3d FTCS 7-point, {G}^3 {args.dtype} grid", "grid": list(N),
-                   "global_batch": 1, "seq_len": G, "parallelism": f"{'slab' if dims[1] == dims[2] == 1 and world > 1 else 'block'} {par}",
+                   "global_batch": 1, "seq_len": G, "parallelism": f"{'slab' if dims[1] == dims[2] == 1 and dims[0] > 1 else 'block'} {par}"
+                   + (f" ({args.virtual_ranks} virtual ranks on 1 GPU)" if args.virtual_ranks > 1 else ""),
                    "kernel": kernel, "graph": not args.no_graph, "overlap": not args.no_overlap},
         "glups_per_gpu": round(value / world, 3),
         "effective_hbm_tbps_per_gpu": round(value / world * 2 * esize / 1e3, 3),

@@ -35,6 +35,10 @@ struct StencilParams {
   double D[3] = {0, 0, 0};  // Dx, Dy, Dz
   DeviceState* state = nullptr;
   int slot = 0;             // residual parity slot
+  // stencil2 only: x range [ux0, ux1) in which the intermediate u = T^{n+1}
+  // is computed (beyond the box on faces with a deep neighbour halo); outside
+  // it u = T^n (Dirichlet ghosts).  ux1 < ux0 means "the box's x range".
+  int64_t ux[2] = {0, -1};
 };
 
 struct InitParams {

@@ -2,7 +2,8 @@
 //
 // One subdomain's field is a single contiguous allocation (no double*** pointer
 // tables: reference heat3D.cu:60-111 / SURVEY.md C5, C15) holding the owned
-// block plus a one-cell ghost shell, z fastest (the reference's T[i][j][k]
+// block plus a one-cell ghost shell (two planes deep in x when the 2-step
+// temporally blocked schedule exchanges deep x halos), z fastest (the reference's T[i][j][k]
 // order, heat3D.cu:394-406).  Rows are padded so that the first owned z point
 // of every row is 128-byte aligned; that lets the stencil kernels issue
 // 16-byte vector loads/stores on gfx950 without realignment.  All indices are
@@ -23,15 +24,17 @@ struct Layout {
   int64_t origin = 0;        // element index of owned (0,0,0)
   int64_t elems = 0;         // allocation length in elements (includes tail pad)
   int64_t esize = 8;
+  int64_t gx = 1;            // ghost planes on each x side (1 or 2)
 
-  // i, j, k in [-1, n] (ghost shell included)
+  // i in [-gx, n0 + gx - 1], j, k in [-1, n] (ghost shell included)
   H3D_HD inline int64_t index(int64_t i, int64_t j, int64_t k) const {
     return origin + i * sx + j * sy + k;
   }
   // Alignment in elements used for the row offset / pitch.
   static int64_t align_elems(int64_t esize) { return 128 / esize; }
-  static Layout make(const int64_t n[3], int64_t esize) {
+  static Layout make(const int64_t n[3], int64_t esize, int64_t gx = 1) {
     Layout L;
+    L.gx = gx;
     for (int a = 0; a < 3; ++a) L.n[a] = n[a];
     L.esize = esize;
     const int64_t A = align_elems(esize);
@@ -41,11 +44,13 @@ struct Layout {
     // break power-of-two row pitches (HBM channel / cache-set aliasing)
     if ((L.sy & (L.sy - 1)) == 0) L.sy += A;
     L.sx = (n[1] + 2) * L.sy;
-    L.origin = L.sx + L.sy + L.zoff;
+    L.origin = gx * L.sx + L.sy + L.zoff;
     // tail pad: kernels may over-read up to one 256-wide z tile past a row end
-    L.elems = (n[0] + 2) * L.sx + 2 * L.sy + 1024;
+    L.elems = (n[0] + 2 * gx) * L.sx + 2 * L.sy + 1024;
     return L;
   }
+  // element offset of the start of x plane i (its ghost row j = -1)
+  H3D_HD inline int64_t plane_offset(int64_t i) const { return (gx + i) * sx; }
   std::size_t bytes() const { return static_cast<std::size_t>(elems * esize); }
 };
 

@@ -1,4 +1,5 @@
 // heat3d-mi355x — CPU backend (OpenMP host kernels, synchronous execution).
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -62,6 +63,10 @@ class CpuBackend final : public Backend {
     std::memcpy(scratch_, p.in, p.L.bytes());
     StencilParams a = p;
     a.out = scratch_;
+    if (p.ux[1] >= p.ux[0]) {  // u on the box's x range widened into deep halos
+      a.box.lo[0] = std::max(p.box.lo[0] - 1, p.ux[0]);
+      a.box.hi[0] = std::min(p.box.hi[0] + 1, p.ux[1]);
+    }
     cpu::stencil(t, a);
     StencilParams b = p;
     b.in = scratch_;

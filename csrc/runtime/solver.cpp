@@ -84,23 +84,46 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   kspec2_.kind = KernelSpec::TB2;
   overlap_ = cfg_.overlap;
 
+  // 2-step temporal blocking: on by default on the GPU, opt-in on the CPU
+  // backend (tests).  Halos may only cross x faces (slabs, or one subdomain)
+  // and travel two planes deep, so every subdomain needs >= 2 owned planes.
+  // Decided from the global decomposition so that every rank agrees.
+  int64_t min_n0 = INT64_MAX;
+  for (const auto& sd : dec_.subs) min_n0 = std::min(min_n0, sd.n[0]);
+  tb2_ = kspec_.kind != KernelSpec::Naive && (cfg_.temporal == 2 || (cfg_.temporal == 0 && be_->is_gpu())) &&
+         dims[1] == 1 && dims[2] == 1 && (dims[0] == 1 || min_n0 >= 2);
+  halo_depth_ = tb2_ && dims[0] > 1 ? 2 : 1;
+  // overlapped pairs need a non-empty interior between the boundary slabs
+  tb2_overlap_ = tb2_ && dims[0] > 1 && overlap_ && min_n0 >= 5;
+
   for (int r : comm_->local_ranks()) {
     Local l;
     l.sd = dec_.subs[r];
-    l.L = Layout::make(l.sd.n, (int64_t)esize_);
+    l.L = Layout::make(l.sd.n, (int64_t)esize_, halo_depth_);
     for (int b = 0; b < 2; ++b) l.field[b] = be_->alloc(l.L.bytes());
     for (int a = 0; a < 3; ++a) {
       l.owned.lo[a] = 0;
       l.owned.hi[a] = l.sd.n[a];
     }
     Decomposition::split_interior(l.sd, &l.interior, &l.shell);
+    const bool lo = l.sd.has_neighbor(Face::Left), hi = l.sd.has_neighbor(Face::Right);
+    l.ux[0] = lo ? -1 : 0;
+    l.ux[1] = l.sd.n[0] + (hi ? 1 : 0);
+    l.tb_interior = l.owned;
+    if (tb2_overlap_) {
+      l.tb_interior.lo[0] = lo ? 2 : 0;
+      l.tb_interior.hi[0] = l.sd.n[0] - (hi ? 2 : 0);
+      for (int side = 0; side < 2; ++side) {
+        if (!(side ? hi : lo)) continue;
+        Box b = l.owned;
+        b.lo[0] = side ? l.sd.n[0] - 2 : 0;
+        b.hi[0] = b.lo[0] + 2;
+        l.tb_boundary.push_back(b);
+      }
+    }
     local_.push_back(l);
   }
   setup_faces();
-  // 2-step temporal blocking: one halo-free subdomain (its ghosts are all
-  // Dirichlet), on by default on the GPU, opt-in on the CPU backend (tests)
-  tb2_ = local_.size() == 1 && !has_halo_ && kspec_.kind != KernelSpec::Naive &&
-         (cfg_.temporal == 2 || (cfg_.temporal == 0 && be_->is_gpu()));
   dstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
   hstate_ = static_cast<DeviceState*>(be_->alloc_host(2 * sizeof(DeviceState)));
   std::memset(hstate_, 0, 2 * sizeof(DeviceState));
@@ -151,10 +174,11 @@ void Solver::setup_faces() {
         io.send_box.lo[b] = io.recv_box.lo[b] = 0;
         io.send_box.hi[b] = io.recv_box.hi[b] = l.sd.n[b];
       }
-      io.send_box.lo[a] = side ? l.sd.n[a] - 1 : 0;
-      io.send_box.hi[a] = io.send_box.lo[a] + 1;
-      io.recv_box.lo[a] = side ? l.sd.n[a] : -1;
-      io.recv_box.hi[a] = io.recv_box.lo[a] + 1;
+      const int64_t dep = a == 0 ? halo_depth_ : 1;
+      io.send_box.lo[a] = side ? l.sd.n[a] - dep : 0;
+      io.send_box.hi[a] = io.send_box.lo[a] + dep;
+      io.recv_box.lo[a] = side ? l.sd.n[a] : -dep;
+      io.recv_box.hi[a] = io.recv_box.lo[a] + dep;
       if (comm_->all_local()) {
         for (std::size_t q = 0; q < local_.size(); ++q)
           if (local_[q].sd.rank == io.peer) io.peer_local = (int)q;
@@ -165,9 +189,9 @@ void Solver::setup_faces() {
         // therefore the same strides.
         io.contiguous = true;
         const int64_t si = io.send_box.lo[0], ri = io.recv_box.lo[0];
-        io.send_off = (si + 1) * l.L.sx;
-        io.recv_off = (ri + 1) * l.L.sx;
-        io.elems = l.L.sx;
+        io.send_off = l.L.plane_offset(si);
+        io.recv_off = l.L.plane_offset(ri);
+        io.elems = dep * l.L.sx;
       } else {
         io.elems = io.send_box.volume();
         io.sendbuf = be_->alloc(io.elems * esize_);
@@ -233,6 +257,7 @@ void Solver::initialize() {
   be_->sync(kCompute);
   issued_ = 0;
   phase_ = 0;
+  last_kind_ = 0;
   segs_.clear();
   seg_head_ = 0;
   if (!cfg_.restart.empty()) load_checkpoint(cfg_.restart);
@@ -323,6 +348,8 @@ void Solver::enqueue_iteration(int p, int bi) {
   auto T = [&](int i, StreamId s) {
     if (phase_timing_) be_->record(tev_[i], s);
   };
+  if (last_kind_ != 1) join_pipeline();
+  last_kind_ = 1;
   // [A] interior sweep on the compute stream
   ev_wait(kCompute, EV_CHK + p);  // convergence check of iteration t-2 (flag + slot reset)
   T(0, kCompute);
@@ -367,35 +394,86 @@ void Solver::enqueue_iteration(int p, int bi) {
   ev_record(EV_CHK + p, kReduce);
 }
 
-// Two iterations t, t+1 (slots p, p^1) as one temporally blocked sweep of the
-// single subdomain: T^t in field[bi] -> T^{t+2} in field[bi^1], both residuals
-// fused, then both convergence checks, all on the compute stream.  The next
-// pair is queued behind those checks, so once converged it is a no-op and
-// field[bi] (T^t) stays intact for the rollback in finalize_converged().
+// Two iterations t, t+1 (slots p, p^1) as one temporally blocked sweep:
+// T^t in field[bi] -> T^{t+2} in field[bi^1], both residuals fused, then both
+// convergence checks.  The next pair is queued behind those checks, so once
+// converged it is a no-op and field[bi] (T^t) stays intact for the rollback
+// in finalize_converged().
+//
+// Single subdomain: everything on the compute stream (graph-capturable).
+// x slabs (pairs alternate buffers, so pipeline events are indexed by bi):
+//   compute: wait check+boundary(prev pair) - interior planes [2, n0-2) - INT
+//   comm   : 2-plane halo of T^t - wait interior+check(prev) - boundary slabs - BND
+//   reduce : wait INT, BND - allreduce(max) of both residual slots - 2 checks - CHK
+// The halo of pair k+1 only depends on pair k's boundary slabs, so it
+// overlaps pair k's interior tail and its all-reduce.
 void Solver::enqueue_double(int p, int bi) {
   H3D_TRACE("double issued=" << issued_ << " parity=" << p << " buf=" << bi
                              << (capturing_ ? " (capturing)" : ""));
-  HEAT3D_CHECK(local_.size() == 1 && !has_halo_, "temporal blocking needs one halo-free subdomain");
-  Local& l = local_[0];
-  ev_wait(kCompute, EV_CHK + 0);
-  ev_wait(kCompute, EV_CHK + 1);
-  StencilParams sp;
-  sp.in = l.field[bi];
-  sp.out = l.field[bi ^ 1];
-  sp.L = l.L;
-  sp.box = l.owned;
-  for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
-  sp.state = dstate_;
-  sp.slot = p;
-  be_->range_push("sweep2");
-  be_->stencil2(dt_, sp, kspec2_, kCompute);
+  HEAT3D_CHECK(tb2_, "temporal blocking not enabled for this decomposition");
+  if (last_kind_ != 2) join_pipeline();
+  last_kind_ = 2;
+  auto params = [&](Local& l, const Box& b) {
+    StencilParams sp;
+    sp.in = l.field[bi];
+    sp.out = l.field[bi ^ 1];
+    sp.L = l.L;
+    sp.box = b;
+    for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+    sp.state = dstate_;
+    sp.slot = p;
+    sp.ux[0] = l.ux[0];
+    sp.ux[1] = l.ux[1];
+    return sp;
+  };
+  auto reduce_and_check = [&](StreamId s) {
+    if (!comm_->all_local() && comm_->size() > 1)
+      comm_->allreduce(&dstate_->residual[0], 2, RedType::U64, RedOp::Max, *be_, s);
+    be_->check_convergence(dstate_, p, s);
+    be_->check_convergence(dstate_, p ^ 1, s);
+  };
+  if (!tb2_overlap_) {
+    ev_wait(kCompute, EV_CHK + 0);
+    ev_wait(kCompute, EV_CHK + 1);
+    if (has_halo_) enqueue_halo(bi, kCompute);
+    be_->range_push("sweep2");
+    for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), kspec2_, kCompute);
+    be_->range_pop();
+    reduce_and_check(kCompute);
+    for (int i = 0; i < 2; ++i) {
+      ev_record(EV_INT + i, kCompute);
+      ev_record(EV_BND + i, kCompute);
+      ev_record(EV_CHK + i, kCompute);
+    }
+    return;
+  }
+  const int q = bi;
+  // [A] interior planes
+  ev_wait(kCompute, EV_CHK + (q ^ 1));  // previous pair's checks: done flag, slots reset
+  ev_wait(kCompute, EV_BND + (q ^ 1));  // its boundary slabs are part of our input
+  be_->range_push("interior2");
+  for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), kspec2_, kCompute);
   be_->range_pop();
-  be_->check_convergence(dstate_, p, kCompute);
-  be_->check_convergence(dstate_, p ^ 1, kCompute);
-  ev_record(EV_INT + 0, kCompute);
-  ev_record(EV_INT + 1, kCompute);
-  ev_record(EV_CHK + 0, kCompute);
-  ev_record(EV_CHK + 1, kCompute);
+  ev_record(EV_INT + q, kCompute);
+  // [B] deep halo, then the boundary slabs
+  enqueue_halo(bi, kComm);
+  ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
+  ev_wait(kComm, EV_CHK + (q ^ 1));
+  be_->range_push("boundary2");
+  for (auto& l : local_)
+    for (const Box& b : l.tb_boundary) be_->stencil2(dt_, params(l, b), kspec2_, kComm);
+  be_->range_pop();
+  ev_record(EV_BND + q, kComm);
+  // [C] both residuals, both checks
+  ev_wait(kReduce, EV_INT + q);
+  ev_wait(kReduce, EV_BND + q);
+  reduce_and_check(kReduce);
+  ev_record(EV_CHK + q, kReduce);
+}
+
+void Solver::join_pipeline() {
+  for (StreamId s : {kCompute, kComm, kReduce})
+    for (int id = EV_INT; id < EV_CHK + 2; ++id) ev_wait(s, id);
 }
 
 void Solver::record_segment(int64_t start, int len, int inbuf) {
@@ -417,15 +495,18 @@ void Solver::finalize_converged(int64_t c) {
   HEAT3D_CHECK(hit, "segment of converged iteration " << c << " not recorded");
   const Segment s = *hit;
   if (s.len == 2 && c == s.start) {
-    Local& l = local_[0];
-    StencilParams sp;
-    sp.in = l.field[s.inbuf];
-    sp.out = l.field[s.inbuf ^ 1];
-    sp.L = l.L;
-    sp.box = l.owned;
-    for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
-    sp.state = nullptr;  // forced: ignores the done flag, no residual
-    be_->stencil(dt_, sp, kspec_, kCompute);
+    // the pair's input buffer still holds T^c with its (1-deep) halo: the
+    // later, no-op pairs only re-exchanged unchanged faces into it
+    for (auto& l : local_) {
+      StencilParams sp;
+      sp.in = l.field[s.inbuf];
+      sp.out = l.field[s.inbuf ^ 1];
+      sp.L = l.L;
+      sp.box = l.owned;
+      for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+      sp.state = nullptr;  // forced: ignores the done flag, no residual
+      be_->stencil(dt_, sp, kspec_, kCompute);
+    }
     be_->sync(kCompute);
   }
   issued_ = c + 1;
@@ -508,7 +589,7 @@ void Solver::run_chunk(int64_t n) {
     return e && e[0] == '1';
   }();
   const bool graphs = cfg_.use_graph && be_->supports_graphs() && comm_->capturable() &&
-                      !graph_failed_ && !phase_timing_ && (!overlap_ || ms_ok);
+                      !graph_failed_ && !phase_timing_ && (!multi_stream() || ms_ok);
   const int want_kind = tb2_ ? 2 : 1;
   while (n > 0) {
     int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
@@ -608,6 +689,8 @@ RunResult Solver::run() {
     if (next_ckpt > 0) n = std::min(n, next_ckpt - issued_);
     run_chunk(n);
     // pinned copy of the device convergence state, polled one chunk later
+    ev_wait(kReduce, EV_CHK + 0);
+    ev_wait(kReduce, EV_CHK + 1);
     be_->copy(&hstate_[pslot], dstate_, poll_bytes, CopyKind::D2H, kReduce);
     ev_record(EV_POLL + pslot, kReduce);
     if (have_prev) {
@@ -917,9 +1000,9 @@ void Solver::load_checkpoint(const std::string& dir) {
 int Solver::verify_halos() {
   be_->sync_all();
   if (issued_ == 0 || !has_halo_) return 0;
-  // input buffer of the last iteration: its ghosts were filled by that
-  // iteration's exchange from the neighbours' (unchanged) faces
-  const int p = cur() ^ 1;  // single-step schedule (halos imply no temporal blocking)
+  // input buffer of the last iteration (or pair): its ghosts were filled by
+  // that exchange from the neighbours' (unchanged) faces
+  const int p = cur() ^ 1;
   int nf = 0;
   for (auto& l : local_) nf += (int)l.faces.size();
   auto* dsum = static_cast<unsigned long long*>(be_->alloc(sizeof(unsigned long long) * 3 * nf));

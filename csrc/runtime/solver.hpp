@@ -96,7 +96,8 @@ class Solver {
   const Layout& local_layout(int i) const { return local_[i].L; }
   // current field buffer of a local subdomain (device pointer on HIP)
   void* local_field_ptr(int i) { return local_[i].field[cur()]; }
-  // True when iterations run as 2-step temporally blocked sweeps.
+  // True when iterations run as 2-step temporally blocked sweeps (single
+  // subdomain, or x slabs with 2-plane halos).
   bool temporal_blocking() const { return tb2_; }
 
   // Output / checkpoint.
@@ -140,6 +141,11 @@ class Solver {
     Box owned, interior;
     std::vector<Box> shell;
     std::vector<FaceIO> faces;
+    // temporally blocked pairs with deep x halos: interior planes [2, n0-2)
+    // (need no halo), 2-plane boundary slabs, u range widened into the halos
+    Box tb_interior;
+    std::vector<Box> tb_boundary;
+    int64_t ux[2] = {0, -1};
   };
 
   void setup_faces();
@@ -148,6 +154,8 @@ class Solver {
   // two iterations in one temporally blocked sweep (single stream)
   void enqueue_double(int p, int bi);
   void enqueue_halo(int bi, StreamId s);
+  void join_pipeline();      // every stream waits for every pipeline event
+  bool multi_stream() const { return tb2_ ? tb2_overlap_ : overlap_; }
   // buffer holding T^{issued_}
   int cur() const { return (int)((issued_ + phase_) & 1); }
   void record_segment(int64_t start, int len, int inbuf);
@@ -168,6 +176,9 @@ class Solver {
   std::vector<Local> local_;
   bool has_halo_ = false;  // any face with a neighbour on any local subdomain
   bool overlap_ = true;
+  bool tb2_overlap_ = false;  // pairs: interior || (deep halo -> boundary slabs)
+  int halo_depth_ = 1;        // x-face halo planes (2 with temporal blocking)
+  int last_kind_ = 0;         // 1 = single step, 2 = pair: last enqueued schedule
   DType dt_;
   std::size_t esize_;
 

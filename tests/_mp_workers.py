@@ -22,14 +22,16 @@ def _init(rank, world, port):
     return dist
 
 
-def native_socket_worker(rank, world, port, outdir, n, eps, decomp, dtype):
+def native_socket_worker(rank, world, port, outdir, n, eps, decomp, dtype, extra_args=()):
     """Native engine, CPU backend, SocketComm bootstrapped through gloo."""
     dist = _init(rank, world, port)
     import heat3d_amd
 
     s = heat3d_amd.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", decomp=decomp, dtype=dtype,
-                              threads=2)
+                              threads=2, extra_args=list(extra_args))
     assert s.native.comm_name == "socket"
+    if "--temporal" in extra_args:
+        assert s.native.temporal_blocking == (extra_args[list(extra_args).index("--temporal") + 1] == "2")
     r = s.run()
     assert s.native.verify_halos() == 0  # checksums exchanged over the socket transport
     g = s.gather()

@@ -7,9 +7,9 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS_F64 = ["tb2", "tb2:2:4:2:4", "tb2:2:4:4:2", "tb2:2:4:1:4", "tb2:2:4:2:2", "tb2:2:8:2:2",
+VARIANTS_F64 = ["tb2", "tb2:2:2:1:8", "tb2:2:2:1:16", "tb2:2:3:1:4", "tb2:2:4:2:4", "tb2:2:4:4:2", "tb2:2:4:1:4", "tb2:2:4:2:2", "tb2:2:8:2:2",
                 "tb2:2:4:2:4:5", "tb2:2:4:2:4:1", "tb2:2:2:2:8"]
-VARIANTS_F32 = ["tb2", "tb2:4:4:2:4", "tb2:4:4:2:2", "tb2:2:4:2:4", "tb2:4:4:2:4:3"]
+VARIANTS_F32 = ["tb2", "tb2:4:2:1:8", "tb2:4:3:1:4", "tb2:4:4:2:4", "tb2:4:4:2:2", "tb2:2:4:2:4", "tb2:4:4:2:4:3"]
 
 
 def _field(ops, n, dtype, gpu, seed):
@@ -74,4 +74,30 @@ def test_temporal_fp32(h3d, gpu):
     b = h3d.HeatSolver((33, 33, 33), 10 ** 6, 1e-4, backend="cpu", dtype="fp32")
     ra, rb = a.run(), b.run()
     assert ra["conv_iter"] == rb["conv_iter"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("vr", [2, 3, 4])
+@pytest.mark.parametrize("overlap", [True, False])
+def test_temporal_slabs_gpu(h3d, gpu, vr, overlap):
+    # x slabs as virtual ranks on one GPU: interior planes on the compute
+    # stream || 2-plane halo + boundary slabs on the comm stream
+    n = (67, 45, 131)
+    a = h3d.HeatSolver(n, 10 ** 6, 1e-4, backend="hip", virtual_ranks=vr, decomp=(vr, 1, 1), overlap=overlap)
+    assert a.native.temporal_blocking
+    b = h3d.HeatSolver(n, 10 ** 6, 1e-4, backend="cpu", extra_args=["--temporal", "1"])
+    ra, rb = a.run(), b.run()
+    assert ra["conv_iter"] == rb["conv_iter"]
+    assert np.array_equal(a.gather(), b.gather())
+    assert a.native.verify_halos() == 0
+
+
+@pytest.mark.parametrize("iters", [3, 50])
+def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
+    n = (70, 33, 64)
+    a = h3d.HeatSolver(n, iters, 0.0, backend="hip", virtual_ranks=4, decomp=(4, 1, 1))
+    b = h3d.HeatSolver(n, iters, 0.0, backend="hip", extra_args=["--temporal", "1"])
+    ra, rb = a.run(), b.run()
+    assert ra["iterations"] == rb["iterations"] == iters
+    assert ra["last_residual"] == rb["last_residual"]
     assert np.array_equal(a.gather(), b.gather())

@@ -64,3 +64,15 @@ def test_torch_reference_matches_native(h3d, tmp_path, world, decomp):
         part = np.load(tmp_path / f"interior_{r}.npy")
         sl = tuple(slice(st[a], st[a] + cnt[a]) for a in range(3))
         assert np.array_equal(part, g[sl]), f"rank {r} differs"
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_socket_temporal_slabs(h3d, tmp_path, world):
+    """2-step temporal blocking across processes: 2-plane x halos over the
+    socket transport, bitwise equal to the single-process single-step solve."""
+    n, eps = 23, 1e-4
+    _spawn(native_socket_worker, world, str(tmp_path), n, eps, (world, 1, 1), "fp64", ["--temporal", "2"])
+    single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", extra_args=["--temporal", "1"])
+    r1 = single.run()
+    assert int(open(tmp_path / "result.txt").read().split()[0]) == r1["conv_iter"]
+    assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
