@@ -88,9 +88,9 @@ std::string Config::usage() {
      << "  --no-overlap              do not split interior/boundary work\n"
      << "  --check-every K           host poll period of the device convergence flag\n"
      << "  --kernel NAME             stencil kernel variant (auto|tile[:V:R:WZ:WY:L]|column|naive)\n"
-     << "  --temporal 0|1|2          2-step temporal blocking (0 auto: on for one halo-free GPU\n"
-     << "                            subdomain; results are bitwise identical)\n"
-     << "  --kernel2 tb2[:V:R:WZ:WY:L]  temporally blocked kernel variant\n"
+     << "  --temporal 0|1|K          K-step temporal blocking, K = 2..6 (0 auto: on on the GPU for\n"
+     << "                            one subdomain or x slabs; 1 off; results are bitwise identical)\n"
+     << "  --kernel2 tbK[:V:R:WZ:WY:L]  temporally blocked kernel variant (tb2, tbk2, tb3..tb6)\n"
      << "  --output PATH|none        Tecplot output (default output/out.dat for small grids)\n"
      << "  --tecplot-layout auto|ref|owned\n"
      << "  --compat                  reproduce reference reporting quirks\n"
@@ -175,7 +175,7 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--kernel2") c.kernel2 = get("--kernel2");
     else if (key == "--temporal") {
       c.temporal = (int)to_i64(get("--temporal"), "--temporal");
-      if (c.temporal < 0 || c.temporal > 2) throw UsageError("--temporal must be 0 (auto), 1 or 2");
+      if (c.temporal < 0 || c.temporal > 6) throw UsageError("--temporal must be 0 (auto), 1 (off) or 2..6");
     }
     else if (key == "--output") c.output = get("--output");
     else if (key == "--tecplot-layout") c.tecplot_layout = get("--tecplot-layout");

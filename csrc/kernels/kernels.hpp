@@ -16,7 +16,8 @@
 namespace heat3d {
 
 struct KernelSpec {
-  enum Kind { Naive = 0, Column = 1, Tile = 2, TB2 = 3 } kind = Tile;
+  enum Kind { Naive = 0, Column = 1, Tile = 2, TB2 = 3, TBK = 4 } kind = Tile;
+  int K = 0;  // TBK: time steps per sweep (TB2 is the tuned K = 2 kernel)
   int WZ = 0, WY = 0;  // tile kernel: waves per workgroup along z and y
   int V = 0;  // elements per lane along z (0 = default for dtype)
   int R = 0;  // rows per wave along y (0 = default)
@@ -34,10 +35,11 @@ struct StencilParams {
   Box box;                  // local owned coordinates to update
   double D[3] = {0, 0, 0};  // Dx, Dy, Dz
   DeviceState* state = nullptr;
-  int slot = 0;             // residual parity slot
-  // stencil2 only: x range [ux0, ux1) in which the intermediate u = T^{n+1}
-  // is computed (beyond the box on faces with a deep neighbour halo); outside
-  // it u = T^n (Dirichlet ghosts).  ux1 < ux0 means "the box's x range".
+  int slot = 0;             // residual slot (multi-step kernels: first of K slots)
+  // multi-step kernels only: x range [ux0, ux1) in which the intermediate
+  // fields T^{n+s} are computed (beyond the box on faces with a deep
+  // neighbour halo); outside it they stay T^n (Dirichlet ghosts).
+  // ux1 < ux0 means "the box's x range".
   int64_t ux[2] = {0, -1};
 };
 
@@ -67,6 +69,8 @@ void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream)
 // residuals of the two steps go to slots p.slot and p.slot ^ 1.  The box must
 // be a whole subdomain whose ghosts are constant (Dirichlet) values.
 void stencil2(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+// K-step temporally blocked sweep (stencil_tbk.hip), K = k.K
+void stencil_multi(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, void* stream);
 void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, void* stream);
 void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
@@ -92,6 +96,12 @@ namespace cpu {
 void set_threads(int n);
 void init_field(DType t, const InitParams& p);
 void stencil(DType t, const StencilParams& p);
+// Definition of the K-step sweep kernels: K single steps through two scratch
+// fields (allocated by the caller, L.bytes() each).  Step s updates the box
+// widened by K-1-s planes into [ux0, ux1) and accumulates into residual slot
+// slot + s (tb2_slots: slot, slot ^ 1, the tuned 2-step kernel's convention).
+void stencil_multi(DType t, const StencilParams& p, int K, bool tb2_slots, void* scratch0,
+                   void* scratch1);
 void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf);
 void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf);
 void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,

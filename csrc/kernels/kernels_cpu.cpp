@@ -22,10 +22,12 @@ template <typename Real>
 static void init_t(const InitParams& p) {
   Real* f = static_cast<Real*>(p.field);
   const Layout& L = p.L;
+  // every ghost plane (deep x halos included) gets its Dirichlet ghost rows
 #pragma omp parallel for collapse(2) schedule(static)
-  for (int64_t i = -1; i <= L.n[0]; ++i)
+  for (int64_t i = -L.gx; i < L.n[0] + L.gx; ++i)
     for (int64_t j = -1; j <= L.n[1]; ++j) {
       const int64_t gi = p.gstart[0] + i, gj = p.gstart[1] + j;
+      if (gi < 0 || gi >= p.N[0]) continue;
       for (int64_t k = -1; k <= L.n[2]; ++k) {
         const int64_t gk = p.gstart[2] + k;
         const bool phys = gi == 0 || gi == p.N[0] - 1 || gj == 0 || gj == p.N[1] - 1 ||
@@ -83,6 +85,27 @@ static void stencil_t(const StencilParams& p) {
   if (p.state) {
     unsigned long long* slot = &p.state->residual[p.slot];
     if (resbits > *slot) *slot = resbits;
+  }
+}
+
+void stencil_multi(DType t, const StencilParams& p, int K, bool tb2_slots, void* scratch0,
+                   void* scratch1) {
+  if (p.state && p.state->done) return;
+  void* scratch[2] = {scratch0, scratch1};
+  std::memcpy(scratch[0], p.in, p.L.bytes());
+  std::memcpy(scratch[1], p.in, p.L.bytes());
+  const bool wide = p.ux[1] >= p.ux[0];
+  for (int s = 0; s < K; ++s) {
+    StencilParams a = p;
+    a.in = s == 0 ? p.in : scratch[(s - 1) & 1];
+    a.out = s == K - 1 ? p.out : scratch[s & 1];
+    a.slot = tb2_slots ? (s ? p.slot ^ 1 : p.slot) : p.slot + s;
+    if (wide) {
+      const int64_t w = K - 1 - s;
+      a.box.lo[0] = std::max(p.box.lo[0] - w, p.ux[0]);
+      a.box.hi[0] = std::min(p.box.hi[0] + w, p.ux[1]);
+    }
+    stencil(t, a);
   }
 }
 

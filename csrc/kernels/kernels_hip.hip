@@ -568,8 +568,9 @@ __global__ __launch_bounds__(256) void init_kernel(Real* f, Layout L, InitParams
   const int64_t ez = L.n[2] + 2;
   const int64_t kk = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (kk >= ez) return;
-  const int64_t k = kk - 1, j = (int64_t)blockIdx.y - 1, i = (int64_t)blockIdx.z - 1;
+  const int64_t k = kk - 1, j = (int64_t)blockIdx.y - 1, i = (int64_t)blockIdx.z - L.gx;
   const int64_t gi = p.gstart[0] + i, gj = p.gstart[1] + j, gk = p.gstart[2] + k;
+  if (gi < 0 || gi >= p.N[0]) return;  // deep ghost plane beyond the domain
   const bool phys = gi == 0 || gi == p.N[0] - 1 || gj == 0 || gj == p.N[1] - 1 || gk == 0 ||
                     gk == p.N[2] - 1;
   f[L.index(i, j, k)] = phys ? (Real)boundary_value(gi, gj, gk, p.N, p.h) : Real(0);
@@ -577,8 +578,9 @@ __global__ __launch_bounds__(256) void init_kernel(Real* f, Layout L, InitParams
 
 void init_field(DType t, const InitParams& p, void* stream) {
   HIPK_CHECK(hipMemsetAsync(p.field, 0, p.L.bytes(), S(stream)));
+  // every ghost plane (deep x halos included) gets its Dirichlet ghost rows
   dim3 grid((unsigned)((p.L.n[2] + 2 + 255) / 256), (unsigned)(p.L.n[1] + 2),
-            (unsigned)(p.L.n[0] + 2));
+            (unsigned)(p.L.n[0] + 2 * p.L.gx));
   if (t == DType::F64)
     hipLaunchKernelGGL(init_kernel<double>, grid, dim3(256), 0, S(stream),
                        static_cast<double*>(p.field), p.L, p);

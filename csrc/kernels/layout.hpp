@@ -58,8 +58,12 @@ struct Layout {
 // subdomain.  The residual accumulators hold the IEEE bit pattern of a
 // non-negative double so that an unsigned 64-bit atomic max (and an RCCL
 // uint64 max all-reduce) is an exact max of the doubles.
+constexpr int kResidualSlots = 8;
+
 struct DeviceState {
-  unsigned long long residual[2];  // per-iteration-parity max |T^{n+1}-T^n|
+  // max |T^{n+1}-T^n| accumulators: single steps use slot t & 1, a K-step
+  // temporally blocked sweep uses slots 0..K-1
+  unsigned long long residual[kResidualSlots];
   double norm;                     // residual of iteration 0 (heat3D.cu:1026-1032)
   double eps;
   double last_residual;

@@ -42,9 +42,9 @@ Box to_box(const std::array<int64_t, 6>& b) {
   return r;
 }
 
-Layout to_layout(const std::array<int64_t, 3>& n, int64_t esize) {
+Layout to_layout(const std::array<int64_t, 3>& n, int64_t esize, int64_t gx = 1) {
   int64_t nn[3] = {n[0], n[1], n[2]};
-  return Layout::make(nn, esize);
+  return Layout::make(nn, esize, gx);
 }
 
 py::dict layout_dict(const Layout& L) {
@@ -56,6 +56,7 @@ py::dict layout_dict(const Layout& L) {
   d["origin"] = L.origin;
   d["elems"] = L.elems;
   d["esize"] = L.esize;
+  d["gx"] = L.gx;
   return d;
 }
 
@@ -213,13 +214,16 @@ PYBIND11_MODULE(_heat3d, m) {
     for (auto& b : shell) sl.append(tup(b));
     return py::make_tuple(tup(in), sl);
   });
-  m.def("layout", [](std::array<int64_t, 3> n, int64_t esize) { return layout_dict(to_layout(n, esize)); });
+  m.def("layout", [](std::array<int64_t, 3> n, int64_t esize, int64_t gx) { return layout_dict(to_layout(n, esize, gx)); },
+        py::arg("n"), py::arg("esize"), py::arg("gx") = 1);
   m.def("boundary_value", [](int64_t i, int64_t j, int64_t k, std::array<int64_t, 3> N, std::array<double, 3> h) {
     int64_t n[3] = {N[0], N[1], N[2]};
     double hh[3] = {h[0], h[1], h[2]};
     return boundary_value(i, j, k, n, hh);
   });
   m.attr("DEVICE_STATE_BYTES") = (int64_t)sizeof(DeviceState);
+  m.attr("RESIDUAL_SLOTS") = (int64_t)kResidualSlots;
+  m.attr("STATE_DONE_OFFSET") = (int64_t)offsetof(DeviceState, done);
   m.attr("RESIDUAL_INIT_BITS") = (unsigned long long)kResidualInitBits;
 
   // --- raw kernels (pointers as ints; stream = hipStream_t as int) ----------
@@ -238,8 +242,28 @@ PYBIND11_MODULE(_heat3d, m) {
     std::array<int64_t, 6> box = {0, n[0], 0, n[1], 0, n[2]};
     auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
     KernelSpec k = KernelSpec::parse(kernel);
-    k.kind = KernelSpec::TB2;
-    hip::stencil2(t, p, k, reinterpret_cast<void*>(stream));
+    if (k.kind == KernelSpec::TBK) {
+      hip::stencil_multi(t, p, k, reinterpret_cast<void*>(stream));
+    } else {
+      k.kind = KernelSpec::TB2;
+      hip::stencil2(t, p, k, reinterpret_cast<void*>(stream));
+    }
+  });
+  // multi-step sweep on a sub-box of a layout with gx ghost planes, u range ux
+  // (the solver's slab path); kernel = tb2 / tbk2 / tb3..tb6 spec
+  hk.def("stencil_sweep", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
+                             int64_t gx, std::array<int64_t, 6> box, std::array<int64_t, 2> ux,
+                             std::array<double, 3> D, int64_t state_ptr, int slot, const std::string& kernel,
+                             int64_t stream) {
+    DType t = dt_of(dt);
+    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
+    p.L = to_layout(n, (int64_t)dtype_size(t), gx);
+    p.ux[0] = ux[0];
+    p.ux[1] = ux[1];
+    KernelSpec k = KernelSpec::parse(kernel);
+    if (k.kind == KernelSpec::TBK) hip::stencil_multi(t, p, k, reinterpret_cast<void*>(stream));
+    else if (k.kind == KernelSpec::TB2) hip::stencil2(t, p, k, reinterpret_cast<void*>(stream));
+    else throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 kernel");
   });
   hk.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
                           std::array<int64_t, 3> N, std::array<double, 3> h, int64_t stream) {
@@ -281,6 +305,21 @@ PYBIND11_MODULE(_heat3d, m) {
     auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
     py::gil_scoped_release nogil;
     cpu::stencil(t, p);
+  });
+  ck.def("stencil_sweep", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
+                             int64_t gx, std::array<int64_t, 6> box, std::array<int64_t, 2> ux,
+                             std::array<double, 3> D, int64_t state_ptr, int slot, const std::string& kernel) {
+    DType t = dt_of(dt);
+    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
+    p.L = to_layout(n, (int64_t)dtype_size(t), gx);
+    p.ux[0] = ux[0];
+    p.ux[1] = ux[1];
+    KernelSpec k = KernelSpec::parse(kernel);
+    if (k.kind != KernelSpec::TB2 && k.kind != KernelSpec::TBK)
+      throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 kernel");
+    std::vector<char> s0(p.L.bytes()), s1(p.L.bytes());
+    py::gil_scoped_release nogil;
+    cpu::stencil_multi(t, p, k.K, k.kind == KernelSpec::TB2, s0.data(), s1.data());
   });
   ck.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
                           std::array<int64_t, 3> N, std::array<double, 3> h) {
@@ -395,6 +434,7 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("iterations_issued", &Solver::iterations_issued)
       .def_property_readonly("kernel_name", &Solver::kernel_name)
       .def_property_readonly("temporal_blocking", &Solver::temporal_blocking)
+      .def_property_readonly("temporal_steps", &Solver::temporal_steps)
       .def_property_readonly("backend_name", [](Solver& s) { return std::string(s.backend().name()); })
       .def_property_readonly("comm_name", [](Solver& s) { return std::string(s.comm().name()); })
       .def_property_readonly("comm_size", [](Solver& s) { return s.comm().size(); })

@@ -51,29 +51,25 @@ class CpuBackend final : public Backend {
   void stencil(DType t, const StencilParams& p, const KernelSpec&, StreamId) override {
     cpu::stencil(t, p);
   }
-  // Reference semantics of the 2-step kernel: two single steps through a
-  // scratch field (same ghosts), residual slots slot and slot^1.
-  void stencil2(DType t, const StencilParams& p, const KernelSpec&, StreamId) override {
+  // Reference semantics of the K-step kernels: K single steps through two
+  // scratch fields (same ghosts).  Step s updates the box widened by K-1-s
+  // planes into [ux0, ux1) and accumulates into residual slot `slot + s`
+  // (tb2: slots slot, slot ^ 1).
+  void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId) override {
     if (p.state && p.state->done) return;
-    if (scratch_bytes_ < p.L.bytes()) {
-      release(scratch_);
-      scratch_ = alloc(p.L.bytes());
-      scratch_bytes_ = p.L.bytes();
-    }
-    std::memcpy(scratch_, p.in, p.L.bytes());
-    StencilParams a = p;
-    a.out = scratch_;
-    if (p.ux[1] >= p.ux[0]) {  // u on the box's x range widened into deep halos
-      a.box.lo[0] = std::max(p.box.lo[0] - 1, p.ux[0]);
-      a.box.hi[0] = std::min(p.box.hi[0] + 1, p.ux[1]);
-    }
-    cpu::stencil(t, a);
-    StencilParams b = p;
-    b.in = scratch_;
-    b.slot = p.slot ^ 1;
-    cpu::stencil(t, b);
+    const int K = k.kind == KernelSpec::TBK ? k.K : 2;
+    for (int i = 0; i < 2; ++i)
+      if (scratch_bytes_[i] < p.L.bytes()) {
+        release(scratch_[i]);
+        scratch_[i] = alloc(p.L.bytes());
+        scratch_bytes_[i] = p.L.bytes();
+      }
+    cpu::stencil_multi(t, p, K, k.kind != KernelSpec::TBK, scratch_[0], scratch_[1]);
   }
-  ~CpuBackend() override { release(scratch_); }
+  ~CpuBackend() override {
+    release(scratch_[0]);
+    release(scratch_[1]);
+  }
   void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, StreamId) override {
     cpu::pack_box(t, f, L, b, buf);
   }
@@ -97,8 +93,8 @@ class CpuBackend final : public Backend {
   }
 
  private:
-  void* scratch_ = nullptr;
-  std::size_t scratch_bytes_ = 0;
+  void* scratch_[2] = {nullptr, nullptr};
+  std::size_t scratch_bytes_[2] = {0, 0};
 
  public:
   void box_bitsum(DType t, const void* f, const Layout& L, const Box& b, unsigned long long* out,

@@ -34,8 +34,13 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     if (parts.size() > 3) k.L = std::atoi(parts[3].c_str());
     if (parts.size() > 4) k.O = std::atoi(parts[4].c_str());
     if (parts.size() > 5) k.NT = std::atoi(parts[5].c_str());
-  } else if (parts[0] == "tile" || parts[0] == "tb2") {
-    k.kind = parts[0] == "tile" ? Tile : TB2;
+  } else if (parts[0] == "tile" || parts[0] == "tb2" || parts[0] == "tbk2" ||
+             (parts[0].size() == 3 && parts[0][0] == 't' && parts[0][1] == 'b' && parts[0][2] >= '3' &&
+              parts[0][2] <= '6')) {
+    // tile = single step; tb2 = tuned 2-step kernel; tb3..tb6 / tbk2 = K-step kernel
+    k.kind = parts[0] == "tile" ? Tile : parts[0] == "tb2" ? TB2 : TBK;
+    if (k.kind == TB2) k.K = 2;
+    if (k.kind == TBK) k.K = parts[0] == "tbk2" ? 2 : parts[0][2] - '0';
     auto at = [&](std::size_t i) { return parts.size() > i ? std::atoi(parts[i].c_str()) : 0; };
     k.V = at(1);
     k.R = at(2);
@@ -45,16 +50,16 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     k.NT = at(6);
   } else {
     throw UsageError("unknown kernel '" + s +
-                     "' (auto | naive | column[:V[:R[:L[:O[:NT]]]]] | tile[:V[:R[:WZ[:WY[:L[:NT]]]]]])");
+                     "' (auto | naive | column[:V[:R[:L[:O[:NT]]]]] | tile|tb2..tb6|tbk2[:V[:R[:WZ[:WY[:L[:NT]]]]]])");
   }
   return k;
 }
 
 std::string KernelSpec::str() const {
   if (kind == Naive) return "naive";
-  if (kind == Tile || kind == TB2) {
+  if (kind == Tile || kind == TB2 || kind == TBK) {
     std::ostringstream os;
-    os << (kind == Tile ? "tile:" : "tb2:") << V << ":" << R << ":" << WZ << ":" << WY << ":" << L
+    os << (kind == Tile ? "tile:" : kind == TB2 ? "tb2:" : K == 2 ? "tbk2:" : "tb" + std::to_string(K) + ":") << V << ":" << R << ":" << WZ << ":" << WY << ":" << L
        << ":" << NT;
     return os.str();
   }
@@ -81,20 +86,33 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   kspec_ = KernelSpec::parse(cfg_.kernel);
   if (kspec_.kind == KernelSpec::TB2) kspec_.kind = KernelSpec::Tile;
   kspec2_ = KernelSpec::parse(cfg_.kernel2);
-  kspec2_.kind = KernelSpec::TB2;
   overlap_ = cfg_.overlap;
 
-  // 2-step temporal blocking: on by default on the GPU, opt-in on the CPU
-  // backend (tests).  Halos may only cross x faces (slabs, or one subdomain)
-  // and travel two planes deep, so every subdomain needs >= 2 owned planes.
-  // Decided from the global decomposition so that every rank agrees.
+  // K-step temporal blocking: on by default on the GPU, opt-in on the CPU
+  // backend (tests).  Depth K from --temporal K, else from --kernel2 tbK,
+  // else kDefaultTemporal.  Halos may only cross x faces (slabs, or one
+  // subdomain) and travel K planes deep, so every subdomain needs >= K owned
+  // planes.  Decided from the global decomposition so that every rank agrees.
+  // Auto depth: 3 for one subdomain; 2 for x slabs, whose K-plane boundary
+  // slabs cost more than the saved traffic at K = 3 (profiles/kernel_sweep.md)
+  int K = cfg_.temporal >= 2 ? cfg_.temporal
+          : (kspec2_.kind == KernelSpec::TB2 || kspec2_.kind == KernelSpec::TBK) ? kspec2_.K
+          : dims[0] > 1 ? 2
+                        : kDefaultTemporal;
+  if (K == 2 && kspec2_.kind != KernelSpec::TBK) {
+    kspec2_.kind = KernelSpec::TB2;
+  } else {
+    kspec2_.kind = KernelSpec::TBK;
+  }
+  kspec2_.K = K;
   int64_t min_n0 = INT64_MAX;
   for (const auto& sd : dec_.subs) min_n0 = std::min(min_n0, sd.n[0]);
-  tb2_ = kspec_.kind != KernelSpec::Naive && (cfg_.temporal == 2 || (cfg_.temporal == 0 && be_->is_gpu())) &&
-         dims[1] == 1 && dims[2] == 1 && (dims[0] == 1 || min_n0 >= 2);
-  halo_depth_ = tb2_ && dims[0] > 1 ? 2 : 1;
-  // overlapped pairs need a non-empty interior between the boundary slabs
-  tb2_overlap_ = tb2_ && dims[0] > 1 && overlap_ && min_n0 >= 5;
+  tb_ = kspec_.kind != KernelSpec::Naive && (cfg_.temporal >= 2 || (cfg_.temporal == 0 && be_->is_gpu())) &&
+        dims[1] == 1 && dims[2] == 1 && (dims[0] == 1 || min_n0 >= K);
+  K_ = tb_ ? K : 1;
+  halo_depth_ = tb_ && dims[0] > 1 ? K : 1;
+  // overlapped sweeps need a non-empty interior between the boundary slabs
+  tb_overlap_ = tb_ && dims[0] > 1 && overlap_ && min_n0 >= 2 * K + 1;
 
   for (int r : comm_->local_ranks()) {
     Local l;
@@ -107,17 +125,17 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     }
     Decomposition::split_interior(l.sd, &l.interior, &l.shell);
     const bool lo = l.sd.has_neighbor(Face::Left), hi = l.sd.has_neighbor(Face::Right);
-    l.ux[0] = lo ? -1 : 0;
-    l.ux[1] = l.sd.n[0] + (hi ? 1 : 0);
+    l.ux[0] = lo ? -(K_ - 1) : 0;
+    l.ux[1] = l.sd.n[0] + (hi ? K_ - 1 : 0);
     l.tb_interior = l.owned;
-    if (tb2_overlap_) {
-      l.tb_interior.lo[0] = lo ? 2 : 0;
-      l.tb_interior.hi[0] = l.sd.n[0] - (hi ? 2 : 0);
+    if (tb_overlap_) {
+      l.tb_interior.lo[0] = lo ? K_ : 0;
+      l.tb_interior.hi[0] = l.sd.n[0] - (hi ? K_ : 0);
       for (int side = 0; side < 2; ++side) {
         if (!(side ? hi : lo)) continue;
         Box b = l.owned;
-        b.lo[0] = side ? l.sd.n[0] - 2 : 0;
-        b.hi[0] = b.lo[0] + 2;
+        b.lo[0] = side ? l.sd.n[0] - K_ : 0;
+        b.hi[0] = b.lo[0] + K_;
         l.tb_boundary.push_back(b);
       }
     }
@@ -246,7 +264,7 @@ void Solver::initialize() {
   }
   DeviceState hs;
   std::memset(&hs, 0, sizeof(hs));
-  hs.residual[0] = hs.residual[1] = kResidualInitBits;
+  for (auto& r : hs.residual) r = kResidualInitBits;
   hs.norm = 1.0;  // heat3D.cu:323-324 (norm = 1 until iteration 0 sets it)
   hs.eps = cfg_.eps;
   hs.iter = 0;
@@ -394,23 +412,22 @@ void Solver::enqueue_iteration(int p, int bi) {
   ev_record(EV_CHK + p, kReduce);
 }
 
-// Two iterations t, t+1 (slots p, p^1) as one temporally blocked sweep:
-// T^t in field[bi] -> T^{t+2} in field[bi^1], both residuals fused, then both
-// convergence checks.  The next pair is queued behind those checks, so once
-// converged it is a no-op and field[bi] (T^t) stays intact for the rollback
-// in finalize_converged().
+// K iterations t..t+K-1 as one temporally blocked sweep: T^t in field[bi]
+// -> T^{t+K} in field[bi^1], the K residuals fused (slots 0..K-1), then the K
+// convergence checks.  The next sweep is queued behind those checks, so once
+// converged it is a no-op and field[bi] (T^t with its halo) stays intact for
+// the rollback in finalize_converged().
 //
 // Single subdomain: everything on the compute stream (graph-capturable).
-// x slabs (pairs alternate buffers, so pipeline events are indexed by bi):
-//   compute: wait check+boundary(prev pair) - interior planes [2, n0-2) - INT
-//   comm   : 2-plane halo of T^t - wait interior+check(prev) - boundary slabs - BND
-//   reduce : wait INT, BND - allreduce(max) of both residual slots - 2 checks - CHK
-// The halo of pair k+1 only depends on pair k's boundary slabs, so it
-// overlaps pair k's interior tail and its all-reduce.
-void Solver::enqueue_double(int p, int bi) {
-  H3D_TRACE("double issued=" << issued_ << " parity=" << p << " buf=" << bi
-                             << (capturing_ ? " (capturing)" : ""));
-  HEAT3D_CHECK(tb2_, "temporal blocking not enabled for this decomposition");
+// x slabs (sweeps alternate buffers, so pipeline events are indexed by bi):
+//   compute: wait check+boundary(prev sweep) - interior planes [K, n0-K) - INT
+//   comm   : K-plane halo of T^t - wait interior+check(prev) - boundary slabs - BND
+//   reduce : wait INT, BND - allreduce(max) of the K residual slots - K checks - CHK
+// The halo of sweep k+1 only depends on sweep k's boundary slabs, so it
+// overlaps sweep k's interior tail and its all-reduce.
+void Solver::enqueue_multi(int bi) {
+  H3D_TRACE("sweep" << K_ << " issued=" << issued_ << " buf=" << bi << (capturing_ ? " (capturing)" : ""));
+  HEAT3D_CHECK(tb_, "temporal blocking not enabled for this decomposition");
   if (last_kind_ != 2) join_pipeline();
   last_kind_ = 2;
   auto params = [&](Local& l, const Box& b) {
@@ -421,37 +438,39 @@ void Solver::enqueue_double(int p, int bi) {
     sp.box = b;
     for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
     sp.state = dstate_;
-    sp.slot = p;
+    sp.slot = 0;
     sp.ux[0] = l.ux[0];
     sp.ux[1] = l.ux[1];
     return sp;
   };
   auto reduce_and_check = [&](StreamId s) {
     if (!comm_->all_local() && comm_->size() > 1)
-      comm_->allreduce(&dstate_->residual[0], 2, RedType::U64, RedOp::Max, *be_, s);
-    be_->check_convergence(dstate_, p, s);
-    be_->check_convergence(dstate_, p ^ 1, s);
+      comm_->allreduce(&dstate_->residual[0], K_, RedType::U64, RedOp::Max, *be_, s);
+    for (int i = 0; i < K_; ++i) be_->check_convergence(dstate_, i, s);
   };
-  if (!tb2_overlap_) {
+  if (!tb_overlap_) {
     ev_wait(kCompute, EV_CHK + 0);
     ev_wait(kCompute, EV_CHK + 1);
     if (has_halo_) enqueue_halo(bi, kCompute);
-    be_->range_push("sweep2");
+    be_->range_push("sweep");
     for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), kspec2_, kCompute);
     be_->range_pop();
     reduce_and_check(kCompute);
-    for (int i = 0; i < 2; ++i) {
-      ev_record(EV_INT + i, kCompute);
-      ev_record(EV_BND + i, kCompute);
-      ev_record(EV_CHK + i, kCompute);
+    if (!capturing_) {
+      for (int i = 0; i < 2; ++i) {
+        ev_record(EV_INT + i, kCompute);
+        ev_record(EV_BND + i, kCompute);
+      }
     }
+    ev_record(EV_CHK + 0, kCompute);
+    ev_record(EV_CHK + 1, kCompute);
     return;
   }
   const int q = bi;
   // [A] interior planes
-  ev_wait(kCompute, EV_CHK + (q ^ 1));  // previous pair's checks: done flag, slots reset
+  ev_wait(kCompute, EV_CHK + (q ^ 1));  // previous sweep's checks: done flag, slots reset
   ev_wait(kCompute, EV_BND + (q ^ 1));  // its boundary slabs are part of our input
-  be_->range_push("interior2");
+  be_->range_push("interior");
   for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), kspec2_, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
@@ -459,12 +478,12 @@ void Solver::enqueue_double(int p, int bi) {
   enqueue_halo(bi, kComm);
   ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
   ev_wait(kComm, EV_CHK + (q ^ 1));
-  be_->range_push("boundary2");
+  be_->range_push("boundary");
   for (auto& l : local_)
     for (const Box& b : l.tb_boundary) be_->stencil2(dt_, params(l, b), kspec2_, kComm);
   be_->range_pop();
   ev_record(EV_BND + q, kComm);
-  // [C] both residuals, both checks
+  // [C] all residuals, all checks
   ev_wait(kReduce, EV_INT + q);
   ev_wait(kReduce, EV_BND + q);
   reduce_and_check(kReduce);
@@ -494,23 +513,34 @@ void Solver::finalize_converged(int64_t c) {
     if (c >= s.start && c < s.start + s.len) hit = &s;
   HEAT3D_CHECK(hit, "segment of converged iteration " << c << " not recorded");
   const Segment s = *hit;
-  if (s.len == 2 && c == s.start) {
-    // the pair's input buffer still holds T^c with its (1-deep) halo: the
-    // later, no-op pairs only re-exchanged unchanged faces into it
-    for (auto& l : local_) {
-      StencilParams sp;
-      sp.in = l.field[s.inbuf];
-      sp.out = l.field[s.inbuf ^ 1];
-      sp.L = l.L;
-      sp.box = l.owned;
-      for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
-      sp.state = nullptr;  // forced: ignores the done flag, no residual
-      be_->stencil(dt_, sp, kspec_, kCompute);
+  const int m = (int)(c - s.start + 1);  // steps of the segment that are wanted
+  int final_buf = s.inbuf ^ 1;
+  if (m < s.len) {
+    // The sweep's input buffer still holds T^start with its K-deep halo (the
+    // later, no-op sweeps only re-exchanged unchanged faces into it).  Redo
+    // m forced single steps; step j also updates m-j halo planes on faces
+    // with a neighbour, so no exchange is needed in between.
+    for (int j = 1; j <= m; ++j) {
+      const int src = (j & 1) ? s.inbuf : s.inbuf ^ 1;
+      for (auto& l : local_) {
+        StencilParams sp;
+        sp.in = l.field[src];
+        sp.out = l.field[src ^ 1];
+        sp.L = l.L;
+        sp.box = l.owned;
+        const int64_t w = m - j;
+        if (l.sd.has_neighbor(Face::Left)) sp.box.lo[0] -= w;
+        if (l.sd.has_neighbor(Face::Right)) sp.box.hi[0] += w;
+        for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+        sp.state = nullptr;  // forced: ignores the done flag, no residual
+        be_->stencil(dt_, sp, kspec_, kCompute);
+      }
     }
     be_->sync(kCompute);
+    final_buf = s.inbuf ^ (m & 1);
   }
   issued_ = c + 1;
-  phase_ = (int)(((s.inbuf ^ 1) - (c + 1)) & 1);
+  phase_ = (int)((final_buf - (c + 1)) & 1);
 }
 
 void Solver::accumulate_phase_times() {
@@ -530,8 +560,8 @@ void Solver::build_graph() {
   // G iterations per graph; temporally blocked graphs hold an even number of
   // pairs so that the buffer roles repeat (G multiple of 4)
   int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
-  if (tb2_) G = std::max(4, G - (G % 4));
-  graph_kind_ = tb2_ ? 2 : 1;
+  if (tb_) G = std::max(2 * K_, G - (G % (2 * K_)));
+  graph_kind_ = tb_ ? 2 : 1;
   graph_parity_ = (int)(issued_ & 1);
   graph_buf_ = cur();
   bool saved[EV_COUNT];
@@ -549,7 +579,7 @@ void Solver::build_graph() {
     ev_wait(kComm, EV_FORK);
     ev_wait(kReduce, EV_FORK);
     if (graph_kind_ == 2) {
-      for (int i = 0; i < G / 2; ++i) enqueue_double(graph_parity_, (graph_buf_ + i) & 1);
+      for (int i = 0; i < G / K_; ++i) enqueue_multi((graph_buf_ + i) & 1);
     } else {
       for (int i = 0; i < G; ++i) enqueue_iteration((graph_parity_ + i) & 1, (graph_buf_ + i) & 1);
     }
@@ -590,10 +620,10 @@ void Solver::run_chunk(int64_t n) {
   }();
   const bool graphs = cfg_.use_graph && be_->supports_graphs() && comm_->capturable() &&
                       !graph_failed_ && !phase_timing_ && (!multi_stream() || ms_ok);
-  const int want_kind = tb2_ ? 2 : 1;
+  const int want_kind = tb_ ? 2 : 1;
   while (n > 0) {
     int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
-    if (tb2_) G = std::max(4, G - (G % 4));
+    if (tb_) G = std::max(2 * K_, G - (G % (2 * K_)));
     if (graph_ && graph_kind_ != want_kind) {
       be_->sync_all();
       be_->destroy_graph(graph_);
@@ -604,12 +634,16 @@ void Solver::run_chunk(int64_t n) {
       if (!graph_) build_graph();
       if (graph_ && (int)(issued_ & 1) == graph_parity_ && cur() == graph_buf_) {
         H3D_TRACE("launch_graph issued=" << issued_);
+        // the graph is launched on the compute stream: order it after work
+        // still pending on the other streams (e.g. an overlapped single step)
+        join_pipeline();
+        last_kind_ = graph_kind_;
         be_->launch_graph(graph_);
         if (graph_kind_ == 2) {
-          for (int i = 0; i < graph_iters_ / 2; ++i) {
-            record_segment(issued_, 2, cur());
-            issued_ += 2;
-            phase_ ^= 1;
+          for (int i = 0; i < graph_iters_ / K_; ++i) {
+            record_segment(issued_, K_, cur());
+            issued_ += K_;
+            phase_ ^= (K_ + 1) & 1;  // a K-step sweep flips the buffer once
           }
         } else {
           for (int i = 0; i < graph_iters_; ++i) {
@@ -626,12 +660,12 @@ void Solver::run_chunk(int64_t n) {
         continue;
       }
     }
-    if (tb2_ && n >= 2 && !phase_timing_) {
-      record_segment(issued_, 2, cur());
-      enqueue_double((int)(issued_ & 1), cur());
-      issued_ += 2;
-      phase_ ^= 1;
-      n -= 2;
+    if (tb_ && n >= K_ && !phase_timing_) {
+      record_segment(issued_, K_, cur());
+      enqueue_multi(cur());
+      issued_ += K_;
+      phase_ ^= (K_ + 1) & 1;  // a K-step sweep flips the buffer once
+      n -= K_;
       continue;
     }
     if (phase_timing_ && !tev_[0])
@@ -675,7 +709,10 @@ RunResult Solver::run() {
   comm_->barrier(*be_);
   be_->sync_all();
   const double t0 = now_s();
-  const int64_t K = std::max(1, cfg_.check_every);
+  // poll chunks hold whole pairs of K-step sweeps, so that temporally blocked
+  // runs stay aligned with their graphs and never fall back to single steps
+  const int64_t K = tb_ ? std::max<int64_t>(2 * K_, cfg_.check_every - cfg_.check_every % (2 * K_))
+                        : std::max(1, cfg_.check_every);
   const std::size_t poll_bytes = cfg_.verbose > 0 ? sizeof(DeviceState) : offsetof(DeviceState, hist);
   int pslot = 0;
   bool have_prev = false, stop = false;
@@ -990,7 +1027,7 @@ void Solver::load_checkpoint(const std::string& dir) {
   hstate_->norm = norm;
   hstate_->done = 0;
   hstate_->conv_iter = -1;
-  hstate_->residual[0] = hstate_->residual[1] = kResidualInitBits;
+  for (auto& r : hstate_->residual) r = kResidualInitBits;
   be_->copy(dstate_, hstate_, sizeof(DeviceState), CopyKind::H2D, kCompute);
   be_->sync(kCompute);
   issued_ = it;

@@ -32,6 +32,10 @@
 
 namespace heat3d {
 
+// Temporal blocking depth used when neither --temporal K nor --kernel2 tbK
+// names one.
+constexpr int kDefaultTemporal = 3;
+
 struct RunResult {
   bool converged = false;
   bool fault = false;
@@ -70,7 +74,7 @@ class Solver {
   int process_rank() const { return local_.empty() ? 0 : local_[0].sd.rank; }
   bool is_root() const;
   int64_t interior_points() const { return (dec_.N[0] - 2) * (dec_.N[1] - 2) * (dec_.N[2] - 2); }
-  std::string kernel_name() const { return tb2_ ? kspec2_.str() + "+" + kspec_.str() : kspec_.str(); }
+  std::string kernel_name() const { return tb_ ? kspec2_.str() + "+" + kspec_.str() : kspec_.str(); }
 
   // (Re)initialise fields: analytic IC/BC (heat3D.cu:408-453) or restart.
   void initialize();
@@ -96,9 +100,10 @@ class Solver {
   const Layout& local_layout(int i) const { return local_[i].L; }
   // current field buffer of a local subdomain (device pointer on HIP)
   void* local_field_ptr(int i) { return local_[i].field[cur()]; }
-  // True when iterations run as 2-step temporally blocked sweeps (single
-  // subdomain, or x slabs with 2-plane halos).
-  bool temporal_blocking() const { return tb2_; }
+  // True when iterations run as K-step temporally blocked sweeps (single
+  // subdomain, or x slabs with K-plane halos); K = temporal_steps().
+  bool temporal_blocking() const { return tb_; }
+  int temporal_steps() const { return K_; }
 
   // Output / checkpoint.
   void write_tecplot(const std::string& path, const std::string& layout);
@@ -141,8 +146,8 @@ class Solver {
     Box owned, interior;
     std::vector<Box> shell;
     std::vector<FaceIO> faces;
-    // temporally blocked pairs with deep x halos: interior planes [2, n0-2)
-    // (need no halo), 2-plane boundary slabs, u range widened into the halos
+    // temporally blocked sweeps with deep x halos: interior planes [K, n0-K)
+    // (need no halo), K-plane boundary slabs, u range widened into the halos
     Box tb_interior;
     std::vector<Box> tb_boundary;
     int64_t ux[2] = {0, -1};
@@ -151,11 +156,11 @@ class Solver {
   void setup_faces();
   // one single-step iteration: residual slot / event parity p, input buffer bi
   void enqueue_iteration(int p, int bi);
-  // two iterations in one temporally blocked sweep (single stream)
-  void enqueue_double(int p, int bi);
+  // K iterations in one temporally blocked sweep from buffer bi
+  void enqueue_multi(int bi);
   void enqueue_halo(int bi, StreamId s);
   void join_pipeline();      // every stream waits for every pipeline event
-  bool multi_stream() const { return tb2_ ? tb2_overlap_ : overlap_; }
+  bool multi_stream() const { return tb_ ? tb_overlap_ : overlap_; }
   // buffer holding T^{issued_}
   int cur() const { return (int)((issued_ + phase_) & 1); }
   void record_segment(int64_t start, int len, int inbuf);
@@ -176,8 +181,8 @@ class Solver {
   std::vector<Local> local_;
   bool has_halo_ = false;  // any face with a neighbour on any local subdomain
   bool overlap_ = true;
-  bool tb2_overlap_ = false;  // pairs: interior || (deep halo -> boundary slabs)
-  int halo_depth_ = 1;        // x-face halo planes (2 with temporal blocking)
+  bool tb_overlap_ = false;   // sweeps: interior || (deep halo -> boundary slabs)
+  int halo_depth_ = 1;        // x-face halo planes (K with temporal blocking)
   int last_kind_ = 0;         // 1 = single step, 2 = pair: last enqueued schedule
   DType dt_;
   std::size_t esize_;
@@ -187,11 +192,12 @@ class Solver {
   int64_t issued_ = 0;              // iterations enqueued so far (absolute index)
   // T^t lives in field[(t + phase_) & 1]; a 2-step sweep flips phase_
   int phase_ = 0;
-  bool tb2_ = false;
+  bool tb_ = false;           // K-step temporal blocking active
+  int K_ = 1;                 // iterations per sweep
   KernelSpec kspec2_;
   struct Segment {
     int64_t start;
-    int len;    // 1 = single step, 2 = temporally blocked pair
+    int len;    // 1 = single step, K = temporally blocked sweep
     int inbuf;  // buffer read by the segment
   };
   std::vector<Segment> segs_;       // ring of recent segments (for convergence rollback)
@@ -211,7 +217,7 @@ class Solver {
   int graph_iters_ = 0;
   int graph_parity_ = 0;
   int graph_buf_ = 0;     // input buffer at the start of the captured chunk
-  int graph_kind_ = 1;    // 1 = single-step iterations, 2 = temporally blocked pairs
+  int graph_kind_ = 1;    // 1 = single-step iterations, 2 = temporally blocked sweeps
   bool graph_failed_ = false;
 
   bool phase_timing_ = false;

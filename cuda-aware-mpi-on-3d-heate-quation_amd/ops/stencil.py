@@ -22,12 +22,13 @@ _DT = {torch.float64: "fp64", torch.float32: "fp32"}
 class PaddedField:
     """One subdomain field in the native padded layout."""
 
-    def __init__(self, n: Sequence[int], dtype=torch.float64, device="cpu"):
+    def __init__(self, n: Sequence[int], dtype=torch.float64, device="cpu", gx: int = 1):
         if dtype not in _DT:
             raise TypeError(f"unsupported dtype {dtype}")
         self.n = tuple(int(v) for v in n)
         self.dtype = dtype
-        self.layout = native().layout(list(self.n), torch.tensor([], dtype=dtype).element_size())
+        self.gx = int(gx)  # ghost planes per x side (deep halos of the K-step slab schedule)
+        self.layout = native().layout(list(self.n), torch.tensor([], dtype=dtype).element_size(), self.gx)
         self.flat = torch.zeros(self.layout["elems"], dtype=dtype, device=device)
 
     @property
@@ -43,6 +44,13 @@ class PaddedField:
         L = self.layout
         off = L["origin"] - L["sx"] - L["sy"] - 1
         shape = tuple(v + 2 for v in self.n)
+        return self.flat.as_strided(shape, (L["sx"], L["sy"], 1), off)
+
+    def deep(self) -> torch.Tensor:
+        """View (n0+2*gx, n1+2, n2+2): every ghost plane plus the y/z ghost shell."""
+        L = self.layout
+        off = L["origin"] - self.gx * L["sx"] - L["sy"] - 1
+        shape = (self.n[0] + 2 * self.gx, self.n[1] + 2, self.n[2] + 2)
         return self.flat.as_strided(shape, (L["sx"], L["sy"], 1), off)
 
     def owned(self) -> torch.Tensor:
@@ -88,11 +96,14 @@ def ftcs_step(src: PaddedField, dst: PaddedField, D: Sequence[float],
 
 def ftcs_step2(src: PaddedField, dst: PaddedField, D: Sequence[float], kernel: str = "auto",
                state: Optional[torch.Tensor] = None, slot: int = 0) -> None:
-    """dst = two FTCS steps of src in ONE temporally blocked sweep (gfx950).
+    """dst = K FTCS steps of src in ONE temporally blocked sweep (gfx950).
 
-    The ghost shell of ``src`` is treated as constant (Dirichlet) for both
-    steps; residuals of the two steps land in ``state`` slots ``slot`` and
-    ``slot ^ 1``.  Bitwise identical to two ``ftcs_step`` calls.
+    ``kernel`` picks the depth: ``tb2[:V:R:WZ:WY:L]`` (tuned 2-step kernel,
+    the default), ``tb3`` .. ``tb6`` or ``tbk2`` (generic K-step kernel,
+    stencil_tbk.hip).  The ghost shell of ``src`` is treated as constant
+    (Dirichlet) for every step; the residual of step s lands in ``state``
+    slot ``slot + s`` (tb2: ``slot`` and ``slot ^ 1``).  Bitwise identical to
+    K ``ftcs_step`` calls.
     """
     if src.layout != dst.layout or src.dtype != dst.dtype or src.device != dst.device:
         raise ValueError("src and dst must share layout, dtype and device")
@@ -105,6 +116,29 @@ def ftcs_step2(src: PaddedField, dst: PaddedField, D: Sequence[float], kernel: s
         sptr = state.data_ptr()
     native().hip.stencil2(src.dt, src.data_ptr(), dst.data_ptr(), list(src.n), list(D), sptr, slot,
                           kernel, _stream_ptr(src.flat))
+
+
+def sweep(src: PaddedField, dst: PaddedField, D: Sequence[float], box: Sequence[int],
+          ux: Sequence[int] = (0, -1), kernel: str = "tb3", state: Optional[torch.Tensor] = None,
+          slot: int = 0) -> None:
+    """One K-step sweep (K from ``kernel``: tb2, tbk2, tb3..tb6) on ``box``
+    = (x0, x1, y0, y1, z0, z1) of a deep-ghost field, with the intermediate
+    steps computed on the x range ``ux`` (the solver's x-slab schedule).
+    GPU tensors run the gfx950 kernel, CPU tensors the K-single-steps
+    definition (csrc/kernels/kernels_cpu.cpp)."""
+    if src.layout != dst.layout or src.dtype != dst.dtype or src.device != dst.device:
+        raise ValueError("src and dst must share layout, dtype and device")
+    sptr = 0
+    if state is not None:
+        if state.device != src.device or state.numel() * state.element_size() < native().DEVICE_STATE_BYTES:
+            raise ValueError("state tensor too small or on the wrong device")
+        sptr = state.data_ptr()
+    args = (src.dt, src.data_ptr(), dst.data_ptr(), list(src.n), src.gx, list(box), list(ux), list(D), sptr, slot,
+            kernel)
+    if src.device.type == "cuda":
+        native().hip.stencil_sweep(*args, _stream_ptr(src.flat))
+    else:
+        native().cpu.stencil_sweep(*args)
 
 
 def init_field(f: PaddedField, gstart: Sequence[int], N: Sequence[int], h: Sequence[float]) -> None:
@@ -148,6 +182,5 @@ def new_state(device, eps: float = 0.0) -> torch.Tensor:
     ext = native()
     st = torch.zeros(ext.DEVICE_STATE_BYTES // 8, dtype=torch.int64)
     init = ext.RESIDUAL_INIT_BITS
-    st[0] = init if init < 2 ** 63 else init - 2 ** 64
-    st[1] = st[0]
+    st[: ext.RESIDUAL_SLOTS] = init if init < 2 ** 63 else init - 2 ** 64
     return st.to(device)

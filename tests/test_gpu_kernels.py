@@ -72,8 +72,7 @@ def test_done_flag_makes_kernel_noop(h3d, gpu, ext):
     out = ops.PaddedField(n, device=gpu)
     out.flat.fill_(3.0)
     state = ops.new_state(gpu)
-    # DeviceState.done lives after residual[2], 5 doubles, iter, conv_iter
-    state.view(torch.int32)[(16 + 5 * 8 + 16) // 4] = 1
+    state.view(torch.int32)[h3d.native().STATE_DONE_OFFSET // 4] = 1
     for v in ("naive", "column", "tile"):
         ops.ftcs_step(dev, out, (0.1, 0.1, 0.1), kernel=v, state=state)
     torch.cuda.synchronize()

@@ -101,3 +101,115 @@ def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
     assert ra["iterations"] == rb["iterations"] == iters
     assert ra["last_residual"] == rb["last_residual"]
     assert np.array_equal(a.gather(), b.gather())
+
+
+VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb3:1:4:1:16", "tb3:1:6:1:8", "tb3:1:4:2:8", "tb3:1:4:1:8:3"],
+              4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1"],
+              2: ["tbk2", "tbk2:2:2:1:8"]}
+
+
+@pytest.mark.parametrize("K", [2, 3, 4])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("n", [(9, 13, 130), (17, 21, 259), (5, 3, 64), (40, 33, 300), (3, 30, 7), (33, 1, 513)])
+def test_stencil_k_bitwise(h3d, gpu, K, dtype, n):
+    ops = h3d.ops
+    D = (0.06, 0.05, 0.04)
+    host, dev = _field(ops, n, dtype, gpu, 5)
+    T = host.ghosted().clone()
+    refs = []
+    for _ in range(K):
+        u, r = ops.ftcs_reference(T, D)
+        T = T.clone()
+        T[1:-1, 1:-1, 1:-1] = u
+        refs.append(r)
+    want = T[1:-1, 1:-1, 1:-1]
+    for v in VARIANTS_K[K]:
+        out = ops.PaddedField(n, dtype=dtype, device=gpu)
+        out.flat.fill_(-3.0)
+        st = ops.new_state(gpu)
+        ops.ftcs_step2(dev, out, D, kernel=v, state=st, slot=0)
+        torch.cuda.synchronize()
+        got = out.owned().cpu()
+        assert torch.equal(got, want), f"{v} {dtype} {n}: max diff {(got - want).abs().max().item()}"
+        for s in range(K):
+            assert ops.residual_from_state(st, s) == refs[s], (v, s)
+
+
+@pytest.mark.parametrize("K", [3, 4])
+@pytest.mark.parametrize("vr,overlap", [(1, True), (3, True), (4, False)])
+def test_temporal_depth_k_solver_gpu(h3d, gpu, K, vr, overlap):
+    n = (67, 45, 131)
+    a = h3d.HeatSolver(n, 10 ** 6, 1e-4, backend="hip", virtual_ranks=vr, decomp=(vr, 1, 1), overlap=overlap,
+                       extra_args=["--temporal", str(K)])
+    assert a.native.temporal_steps == K
+    b = h3d.HeatSolver(n, 10 ** 6, 1e-4, backend="cpu", extra_args=["--temporal", "1"])
+    ra, rb = a.run(), b.run()
+    assert ra["conv_iter"] == rb["conv_iter"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("K", [3, 4])
+def test_temporal_depth_k_goldens(h3d, gpu, K):
+    for n, eps in ((27, 1e-3), (33, 1e-5), (64, 1e-3)):
+        it, err, _ = h3d.utils.golden(n, eps)
+        r = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="hip", extra_args=["--temporal", str(K)]).run()
+        assert r["conv_iter"] == it and abs(r["error_percent"] - err) < 6e-5, (K, n, eps, r)
+
+
+def _deep_random(ops, n, gx, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    f = ops.PaddedField(n, dtype=dtype, gx=gx)
+    f.deep().copy_(torch.rand(f.deep().shape, generator=g, dtype=torch.float64).to(dtype))
+    return f
+
+
+@pytest.mark.parametrize("kernel", ["tb2", "tbk2", "tb3", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb4", "tb4:1:6:1:8"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (5, (0, 5), "lo"), (9, (0, 9), "hi"),
+                                            (12, (4, 8), "both"), (12, (0, 4), "both"), (12, (8, 12), "both"),
+                                            (30, (0, 30), "both")])
+def test_sweep_deep_halo_matches_cpu(h3d, gpu, kernel, dtype, n0, box_x, side):
+    """The slab path: K-plane ghost layers, u range widened into them, thin
+    and partial x boxes.  gfx950 sweep == CPU K-single-steps definition."""
+    ops = h3d.ops
+    head = kernel.split(":")[0]
+    K = 2 if head in ("tb2", "tbk2") else int(head[2])
+    n = (n0, 37, 133)
+    ux = (-(K - 1) if side in ("lo", "both") else 0, n0 + (K - 1 if side in ("hi", "both") else 0))
+    box = (box_x[0], box_x[1], 0, n[1], 0, n[2])
+    D = (0.06, 0.05, 0.04)
+    src = _deep_random(ops, n, K, dtype, 7)
+    want = ops.PaddedField(n, dtype=dtype, gx=K)
+    want.flat.fill_(-5.0)
+    st_c = ops.new_state("cpu")
+    ops.sweep(src, want, D, box, ux, kernel=kernel, state=st_c)
+    dsrc = ops.PaddedField(n, dtype=dtype, device=gpu, gx=K)
+    dsrc.flat.copy_(src.flat)
+    got = ops.PaddedField(n, dtype=dtype, device=gpu, gx=K)
+    got.flat.fill_(-5.0)
+    st_g = ops.new_state(gpu)
+    ops.sweep(dsrc, got, D, box, ux, kernel=kernel, state=st_g)
+    torch.cuda.synchronize()
+    x0, x1 = box_x
+    a = got.owned().cpu()[x0:x1]
+    b = want.owned()[x0:x1]
+    assert torch.equal(a, b), f"{kernel} {n0} {box_x} {side}: max diff {(a - b).abs().max().item()}"
+    for s in range(K):
+        assert ops.residual_from_state(st_g, s) == ops.residual_from_state(st_c, s), (kernel, s)
+
+
+@pytest.mark.parametrize("K,vr", [(3, 8), (3, 1), (2, 4), (4, 3)])
+def test_temporal_mixed_steps_gpu(h3d, gpu, K, vr):
+    # single steps (3-stream overlapped schedule) interleaved with K-step
+    # sweeps and their hipGraphs: every hand-over must be stream-ordered
+    n = (37, 37, 70)
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="hip", virtual_ranks=vr, decomp=(vr, 1, 1),
+                       graph_chunk=12, extra_args=["--temporal", str(K)])
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", extra_args=["--temporal", "1"])
+    a.initialize(), b.initialize()
+    for k in (1, 31, 2, 64, 5, 60, 7, 24):
+        a.step(k)
+        b.step(k)
+    a.synchronize()
+    assert a.state()["iter"] == b.state()["iter"] == 194
+    assert np.array_equal(a.gather(), b.gather())

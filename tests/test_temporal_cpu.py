@@ -1,21 +1,46 @@
-"""2-step temporal blocking with x-slab decompositions (2-plane halos), CPU
-backend: the pair schedule (interior planes || deep halo -> boundary slabs,
+"""K-step temporal blocking with x-slab decompositions (K-plane halos), CPU
+backend: the sweep schedule (interior planes || deep halo -> boundary slabs,
 convergence rollback) must reproduce the single-step solver bit for bit for
-every slab count, overlap mode and iteration count.  The CPU backend's
-stencil2 is the two-single-steps definition of the gfx950 kernel."""
+every depth K, slab count, overlap mode and iteration count.  The CPU
+backend's multi-step sweep is the K-single-steps definition of the gfx950
+kernels (stencil_tb2.hip, stencil_tbk.hip)."""
 import numpy as np
 import pytest
 
 T2 = ["--temporal", "2"]
 T1 = ["--temporal", "1"]
+DEPTHS = [2, 3, 4]
 
 
-def _pair(h3d, n, iters, eps, vr, overlap=True, extra=()):
+def _pair(h3d, n, iters, eps, vr, overlap=True, extra=(), K=2):
     a = h3d.HeatSolver(n, iters, eps, backend="cpu", virtual_ranks=vr, decomp=(vr, 1, 1),
-                       overlap=overlap, extra_args=T2 + list(extra))
+                       overlap=overlap, extra_args=["--temporal", str(K)] + list(extra))
     b = h3d.HeatSolver(n, iters, eps, backend="cpu", extra_args=T1)
     assert a.native.temporal_blocking and not b.native.temporal_blocking
+    assert a.native.temporal_steps == K
     return a, b
+
+
+@pytest.mark.parametrize("K", DEPTHS)
+@pytest.mark.parametrize("vr", [1, 2, 3])
+@pytest.mark.parametrize("iters", [1, 5, 17])
+def test_depth_k_matches_single_step(h3d, K, vr, iters):
+    a, b = _pair(h3d, (37, 17, 19), iters, 0.0, vr, K=K)
+    ra, rb = a.run(), b.run()
+    assert ra["iterations"] == rb["iterations"] == iters
+    assert ra["last_residual"] == rb["last_residual"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("K", [3, 4])
+@pytest.mark.parametrize("vr", [1, 3])
+def test_depth_k_convergence_rollback(h3d, K, vr):
+    # converged iteration lands at every offset inside a K-sweep
+    for eps in (1e-3, 9e-4, 8e-4, 7e-4):
+        a, b = _pair(h3d, (25, 25, 25), 10 ** 6, eps, vr, K=K, extra=["--check-every", "5"])
+        ra, rb = a.run(), b.run()
+        assert ra["conv_iter"] == rb["conv_iter"] and ra["converged"]
+        assert np.array_equal(a.gather(), b.gather()), (K, vr, eps, rb["conv_iter"])
 
 
 @pytest.mark.parametrize("vr", [2, 3, 4])
@@ -78,3 +103,28 @@ def test_slab_pairs_odd_steps_and_state(h3d):
     a.synchronize(), b.synchronize()
     assert a.state()["iter"] == b.state()["iter"] == 17
     assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("K", [2, 3, 4])
+@pytest.mark.parametrize("box_x,ux", [((0, 6), (-1, 7)), ((2, 4), (-3, 9)), ((0, 3), (0, 8)), ((3, 6), (-2, 6))])
+def test_cpu_sweep_definition(h3d, K, box_x, ux):
+    """ops.sweep on the CPU (the definition the gfx950 kernels are tested
+    against) == K plain-torch steps on shrinking widened x ranges."""
+    import torch
+    ops = h3d.ops
+    n = (6, 7, 9)
+    ux = (max(ux[0], -(K - 1)), min(ux[1], n[0] + K - 1))
+    g = torch.Generator().manual_seed(3)
+    f = ops.PaddedField(n, gx=K)
+    f.deep().copy_(torch.rand(f.deep().shape, generator=g, dtype=torch.float64))
+    out = ops.PaddedField(n, gx=K)
+    ops.sweep(f, out, (0.07, 0.05, 0.03), (box_x[0], box_x[1], 0, n[1], 0, n[2]), ux,
+              kernel="tb2" if K == 2 else f"tb{K}")
+    T = f.deep().clone()  # plane index i <-> T[i + K]
+    for s in range(K):
+        w = K - 1 - s
+        lo, hi = max(box_x[0] - w, ux[0]), min(box_x[1] + w, ux[1])
+        new, _ = ops.ftcs_reference(T[lo + K - 1: hi + K + 1], (0.07, 0.05, 0.03))
+        T = T.clone()
+        T[lo + K: hi + K, 1:-1, 1:-1] = new
+    assert torch.equal(out.owned()[box_x[0]:box_x[1]], T[box_x[0] + K: box_x[1] + K, 1:-1, 1:-1])
