@@ -34,6 +34,9 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--grid", type=int, default=1024)
+    ap.add_argument("--weak-block", type=int, default=0,
+                    help="weak scaling: each GPU owns B^3 interior points, global grid = dims*B + 2 "
+                         "(BASELINE config 5: B=2047 fp32 gives 4096^3 on 8 GPUs)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--decomp", default="auto", help="auto | slab | block | AxBxC")
     ap.add_argument("--kernel", default="auto")
@@ -42,7 +45,7 @@ def main() -> int:
     ap.add_argument("--graph-chunk", type=int, default=32)
     ap.add_argument("--converge-eps", type=float, default=1e-3,
                     help="also measure time-to-converge at this EPS (0 disables)")
-    ap.add_argument("--temporal", type=int, default=0, help="0 auto | 1 single-step | 2 two-step pairs")
+    ap.add_argument("--temporal", type=int, default=0, help="0 auto | 1 single-step | K (2..6) K-step temporally blocked sweeps")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: split the grid into this many subdomains on one GPU (not the headline)")
     ap.add_argument("--json-out", default="")
@@ -73,14 +76,17 @@ def main() -> int:
 
     G = args.grid
     N = (G, G, G)
-    if args.decomp in ("auto", "slab", "block"):
-        dims = best_dims_for(N, world, None if args.decomp == "auto" else args.decomp)
-    else:
-        dims = tuple(int(v) for v in args.decomp.lower().split("x"))
+    nparts = world * args.virtual_ranks
     if args.virtual_ranks > 1:
         assert world == 1, "--virtual-ranks is a single-process diagnostic"
-        dims = best_dims_for(N, args.virtual_ranks, None if args.decomp == "auto" else args.decomp)
-    assert dims[0] * dims[1] * dims[2] == world * args.virtual_ranks
+    if args.decomp in ("auto", "slab", "block"):
+        dims = best_dims_for(N, nparts, None if args.decomp == "auto" else args.decomp)
+    else:
+        dims = tuple(int(v) for v in args.decomp.lower().split("x"))
+    assert dims[0] * dims[1] * dims[2] == nparts, (dims, nparts)
+    if args.weak_block:
+        N = tuple(d * args.weak_block + 2 for d in dims)
+        G = N[0]
 
     def make(eps, iter_max):
         return HeatSolver(N, iter_max=iter_max, eps=eps, dtype=args.dtype, backend="hip",
@@ -132,11 +138,12 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if args.weak_block else "strong",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (analytic Dirichlet IC/BC of the reference, random-free)",
-        "config": {"model": f"heat3d FTCS 7-point, {G}^3 {args.dtype} grid", "grid": list(N),
+        "config": {"model": f"heat3d FTCS 7-point, {'x'.join(map(str, N)) if len(set(N)) > 1 else f'{G}^3'} {args.dtype} grid",
+                   "grid": list(N),
                    "global_batch": 1, "seq_len": G, "parallelism": f"{'slab' if dims[1] == dims[2] == 1 and dims[0] > 1 else 'block'} {par}"
                    + (f" ({args.virtual_ranks} virtual ranks on 1 GPU)" if args.virtual_ranks > 1 else ""),
                    "kernel": kernel, "graph": not args.no_graph, "overlap": not args.no_overlap},
