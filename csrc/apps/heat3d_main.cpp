@@ -12,11 +12,55 @@
 #include <exception>
 #include <iostream>
 
+#include "../compat/reference_scheme.hpp"
 #include "../core/config.hpp"
+#include "../core/decomp.hpp"
 #include "../io/io.hpp"
 #include "../runtime/solver.hpp"
 
 using namespace heat3d;
+
+// --scheme reference: the reference's own decomposition, emulated in-process
+// (SURVEY.md App. B.3b); report lines as the reference printed them.
+static int run_reference_scheme(const Config& cfg) {
+  const int P = cfg.virtual_ranks;
+  std::array<int, 3> dims = cfg.decomp;
+  if (dims[0] * dims[1] * dims[2] == 0) dims = dims_create(P, dims);
+  ReferenceScheme rs(cfg.n, dims);
+  if (!cfg.quiet) std::cout << cfg.echo_banner() << std::flush;
+  ReferenceSchemeResult r = rs.run(cfg.iter_max, cfg.eps, cfg.verbose);
+  std::printf("Computational time (parallel): %.6f\n\n", r.seconds);
+  if (r.converged)
+    std::printf("Simulation has converged in %lld iterations with a convergence threshold of %e\n",
+                (long long)r.conv_iter, cfg.eps);
+  else
+    std::printf("Simulation did not converge within %lld iterations.\n", (long long)cfg.iter_max);
+  std::printf("L2-norm error: %.4f %%\n", 100.0 * r.error_rank0);
+  std::printf("heat3d: scheme=reference ranks=%d dims=%dx%dx%d chunk=%lldx%lldx%lld norm_rank0=%.6e "
+              "global_error=%.4f%%\n",
+              rs.ranks(), dims[0], dims[1], dims[2], (long long)rs.chunk()[0], (long long)rs.chunk()[1],
+              (long long)rs.chunk()[2], r.norm_rank0, 100.0 * r.error_global);
+  std::fflush(stdout);
+  std::string out = cfg.output;
+  const double pts = (double)cfg.n[0] * cfg.n[1] * cfg.n[2];
+  if (out == "auto") out = pts <= 2.2e6 ? "output/out.dat" : "none";
+  if (out != "none") rs.write_tecplot(out);
+  if (!cfg.json_out.empty()) {
+    io::Json j;
+    j.set("scheme", std::string("reference"));
+    j.set_raw("dims", "[" + std::to_string(dims[0]) + ", " + std::to_string(dims[1]) + ", " +
+                          std::to_string(dims[2]) + "]");
+    j.set_bool("converged", r.converged);
+    j.set("conv_iter", (int64_t)r.conv_iter);
+    j.set("iterations", (int64_t)r.iterations);
+    j.set("seconds", r.seconds);
+    j.set("norm_rank0", r.norm_rank0);
+    j.set("error_percent_rank0_local", 100.0 * r.error_rank0);
+    j.set("error_percent_global", 100.0 * r.error_global);
+    io::write_file_atomic(cfg.json_out, j.dump() + "\n");
+  }
+  return 0;
+}
 
 int main(int argc, char** argv) {
   Config cfg;
@@ -31,6 +75,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   try {
+    if (cfg.scheme == "reference") return run_reference_scheme(cfg);
     auto solver = make_solver_from_env(cfg);
     const bool root = solver->is_root();
     if (root && !cfg.quiet) std::cout << cfg.echo_banner() << std::flush;

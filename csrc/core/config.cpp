@@ -94,6 +94,9 @@ std::string Config::usage() {
      << "  --output PATH|none        Tecplot output (default output/out.dat for small grids)\n"
      << "  --tecplot-layout auto|ref|owned\n"
      << "  --compat                  reproduce reference reporting quirks\n"
+     << "  --scheme ghost|reference  reference: emulate the reference's shared-plane decomposition\n"
+     << "                            (edge extrapolation, corner averaging, local norm, any-rank\n"
+     << "                            stop; CPU, all ranks of --decomp / --virtual-ranks in-process)\n"
      << "  --checkpoint-every K --checkpoint-dir DIR   periodic binary checkpoints\n"
      << "  --restart DIR             resume from a checkpoint directory\n"
      << "  --json-out PATH           write a JSON run report\n"
@@ -180,6 +183,11 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--output") c.output = get("--output");
     else if (key == "--tecplot-layout") c.tecplot_layout = get("--tecplot-layout");
     else if (key == "--compat") c.compat = true;
+    else if (key == "--scheme") {
+      c.scheme = get("--scheme");
+      if (c.scheme != "ghost" && c.scheme != "reference")
+        throw UsageError("--scheme must be ghost or reference");
+    }
     else if (key == "--checkpoint-every") c.checkpoint_every = to_i64(get("--checkpoint-every"), "--checkpoint-every");
     else if (key == "--verify-halo") c.verify_halo = to_i64(get("--verify-halo"), "--verify-halo");
     else if (key == "--timers") c.timers = true;

@@ -55,6 +55,9 @@ struct Config {
   std::string output = "auto";            // path | none | auto (output/out.dat when small)
   std::string tecplot_layout = "auto";    // auto | ref | owned
   bool compat = false;                    // reproduce reference reporting quirks
+  // "ghost": this framework's decomposition (default); "reference": emulate
+  // the reference's shared-plane scheme (compat/reference_scheme.hpp, CPU)
+  std::string scheme = "ghost";
   int64_t checkpoint_every = 0;
   int64_t verify_halo = 0;                // race detection: checksum halos every K iterations
   bool timers = false;                    // per-phase timing (synchronised diagnostic run)

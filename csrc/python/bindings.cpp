@@ -19,6 +19,7 @@
 #include "../comm/net.hpp"
 #include "../core/config.hpp"
 #include "../core/decomp.hpp"
+#include "../compat/reference_scheme.hpp"
 #include "../runtime/solver.hpp"
 
 namespace py = pybind11;
@@ -336,6 +337,39 @@ PYBIND11_MODULE(_heat3d, m) {
   });
 
   // --- solver ---------------------------------------------------------------
+  py::class_<ReferenceScheme>(m, "ReferenceScheme",
+                              "The reference's shared-plane decomposition scheme, all ranks in-process (CPU)")
+      .def(py::init([](std::array<int64_t, 3> N, std::array<int, 3> dims) {
+             int64_t n[3] = {N[0], N[1], N[2]};
+             return new ReferenceScheme(n, dims);
+           }),
+           py::arg("N"), py::arg("dims"))
+      .def_property_readonly("chunk", [](const ReferenceScheme& r) { return r.chunk(); })
+      .def_property_readonly("ranks", &ReferenceScheme::ranks)
+      .def("run", [](ReferenceScheme& rs, int64_t iter_max, double eps) {
+             ReferenceSchemeResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = rs.run(iter_max, eps);
+             }
+             py::dict d;
+             d["converged"] = r.converged;
+             d["conv_iter"] = r.conv_iter;
+             d["iterations"] = r.iterations;
+             d["seconds"] = r.seconds;
+             d["norm_rank0"] = r.norm_rank0;
+             d["error_percent_rank0"] = 100.0 * r.error_rank0;
+             d["error_percent_global"] = 100.0 * r.error_global;
+             d["last_residual_rank0"] = r.last_residual_rank0;
+             return d;
+           },
+           py::arg("iter_max"), py::arg("eps"))
+      .def("gather", [](const ReferenceScheme& rs) {
+        auto g = rs.gather();
+        return py::array_t<double>(g.size(), g.data());
+      })
+      .def("write_tecplot", &ReferenceScheme::write_tecplot);
+
   py::class_<Solver>(m, "Solver")
       .def(py::init(&create_solver), py::arg("args"), py::arg("rank") = 0, py::arg("size") = 1,
            py::arg("comm") = "local", py::arg("unique_id") = py::bytes(), py::arg("listen_fd") = -1,
