@@ -26,6 +26,9 @@ struct KernelSpec {
   int NT = 0; // non-temporal output stores
   static KernelSpec parse(const std::string& s);
   std::string str() const;
+  // zero (default) fields replaced by the tuned defaults for dtype t
+  // (profiles/kernel_sweep.md); the kernel dispatchers and kernel names use it
+  KernelSpec resolved(DType t) const;
 };
 
 struct StencilParams {

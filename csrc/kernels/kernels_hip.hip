@@ -497,9 +497,9 @@ static void launch_column(const StencilParams& p, const KernelSpec& k, hipStream
 }
 
 template <typename Real>
-static void dispatch_column(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
-  const int V = k.V ? k.V : (sizeof(Real) == 8 ? 2 : 4);
-  const int R = k.R ? k.R : 8;
+static void dispatch_column(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
+  const KernelSpec k = ks.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
+  const int V = k.V, R = k.R;
   // Thin boxes (boundary shell slabs) go to the naive kernel: a column tile
   // would run mostly idle lanes / rows there.
   if (p.box.extent(2) < 32 || p.box.extent(1) < 2) {
@@ -522,12 +522,10 @@ static void dispatch_column(const StencilParams& p, const KernelSpec& k, hipStre
 }
 
 template <typename Real>
-static void dispatch_tile(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
-  // defaults from the gfx950 sweep (profiles/kernel_sweep.md): 8-wave tiles,
-  // 16 rows x 512 points fp64, 16 rows x 512 points fp32
-  const int V = k.V ? k.V : (sizeof(Real) == 8 ? 2 : 4);
-  const int R = k.R ? k.R : 8;
-  const int WZ = k.WZ ? k.WZ : (sizeof(Real) == 8 ? 4 : 2), WY = k.WY ? k.WY : 2;
+static void dispatch_tile(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
+  // defaults from the gfx950 sweep (KernelSpec::resolved, profiles/kernel_sweep.md)
+  const KernelSpec k = ks.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
+  const int V = k.V, R = k.R, WZ = k.WZ, WY = k.WY;
   if (p.box.extent(2) < 32 || p.box.extent(1) < 2) {
     launch_naive<Real>(p, s);
     return;

@@ -304,12 +304,10 @@ static void launch_tb2(const StencilParams& p, const KernelSpec& k, hipStream_t 
 
 template <typename Real>
 static void dispatch_tb2(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
-  // defaults from the MI355X sweep (profiles/kernel_sweep.md): one wave per
-  // tile column, 8 waves of 2 rows stacked in y (~100 VGPRs: 2 blocks/CU)
-  const bool f64 = sizeof(Real) == 8;
-  const int V = k.V ? k.V : (f64 ? 2 : 4);
-  const int R = k.R ? k.R : 2;
-  const int WZ = k.WZ ? k.WZ : 1, WY = k.WY ? k.WY : 8;
+  // defaults (KernelSpec::resolved) from the MI355X sweep: one wave per tile
+  // column, 8 waves of 2 rows stacked in y (~100 VGPRs: 2 blocks/CU)
+  const KernelSpec r = k.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
+  const int V = r.V, R = r.R, WZ = r.WZ, WY = r.WY;
 #define H3D_TB2(VV, RR, ZZ, YY)                      \
   if (V == VV && R == RR && WZ == ZZ && WY == YY) {  \
     launch_tb2<Real, VV, RR, ZZ, YY>(p, k, s);       \

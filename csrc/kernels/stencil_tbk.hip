@@ -390,13 +390,11 @@ static void launch_tbk(const StencilParams& p, const KernelSpec& ks, hipStream_t
 
 template <typename Real>
 static void dispatch_tbk(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
-  const bool f64 = sizeof(Real) == 8;
   const int K = k.K;
-  // defaults from the MI355X sweep (profiles/kernel_sweep.md)
-  const int V = k.V ? k.V : (f64 ? 1 : 2);
-  const int R = k.R ? k.R : 4;
-  const int WZ = k.WZ ? k.WZ : 1, WY = k.WY ? k.WY : (f64 ? 16 : 8);
-  const int PD = k.NT ? k.NT : 1;  // 7th spec field: prefetch depth in planes
+  // defaults (KernelSpec::resolved) from the MI355X sweep (profiles/kernel_sweep.md)
+  const KernelSpec r = k.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
+  const int V = r.V, R = r.R, WZ = r.WZ, WY = r.WY;
+  const int PD = r.NT;  // 7th spec field: prefetch depth in planes
 #define H3D_TBK(VV, RR, ZZ, YY, KK, PP)                                     \
   if (V == VV && R == RR && WZ == ZZ && WY == YY && K == KK && PD == PP) {  \
     launch_tbk<Real, VV, RR, ZZ, YY, KK, PP>(p, k, s);                      \

@@ -55,6 +55,42 @@ KernelSpec KernelSpec::parse(const std::string& s) {
   return k;
 }
 
+KernelSpec KernelSpec::resolved(DType t) const {
+  KernelSpec r = *this;
+  const bool f64 = t == DType::F64;
+  auto def = [](int& f, int v) {
+    if (f == 0) f = v;
+  };
+  switch (kind) {
+    case Column:
+      def(r.V, f64 ? 2 : 4);
+      def(r.R, 8);
+      break;
+    case Tile:  // 8-wave tiles, 16 rows x 512 points
+      def(r.V, f64 ? 2 : 4);
+      def(r.R, 8);
+      def(r.WZ, f64 ? 4 : 2);
+      def(r.WY, 2);
+      break;
+    case TB2:  // one wave per tile column, 8 waves of 2 rows
+      def(r.V, f64 ? 2 : 4);
+      def(r.R, 2);
+      def(r.WZ, 1);
+      def(r.WY, 8);
+      break;
+    case TBK:  // 64-row tiles of 16 waves (fp64, V=1) / 32-row tiles of 8 waves (fp32)
+      def(r.V, f64 ? 1 : 2);
+      def(r.R, 4);
+      def(r.WZ, 1);
+      def(r.WY, f64 ? 16 : 8);
+      def(r.NT, 1);  // prefetch depth
+      break;
+    default:
+      break;
+  }
+  return r;
+}
+
 std::string KernelSpec::str() const {
   if (kind == Naive) return "naive";
   if (kind == Tile || kind == TB2 || kind == TBK) {

@@ -74,7 +74,10 @@ class Solver {
   int process_rank() const { return local_.empty() ? 0 : local_[0].sd.rank; }
   bool is_root() const;
   int64_t interior_points() const { return (dec_.N[0] - 2) * (dec_.N[1] - 2) * (dec_.N[2] - 2); }
-  std::string kernel_name() const { return tb_ ? kspec2_.str() + "+" + kspec_.str() : kspec_.str(); }
+  std::string kernel_name() const {
+    const std::string one = kspec_.resolved(cfg_.dtype).str();
+    return tb_ ? kspec2_.resolved(cfg_.dtype).str() + "+" + one : one;
+  }
 
   // (Re)initialise fields: analytic IC/BC (heat3D.cu:408-453) or restart.
   void initialize();
