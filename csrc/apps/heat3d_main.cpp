@@ -7,15 +7,20 @@
 // Multi-process runs read RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR /
 // MASTER_PORT (torchrun or mpirun env); every rank validates the command line
 // (the reference only checked argc on rank 0).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
 #include <iostream>
+#include <thread>
+#include <vector>
 
 #include "../compat/reference_scheme.hpp"
 #include "../core/config.hpp"
 #include "../core/decomp.hpp"
+#include "../comm/comm.hpp"
 #include "../io/io.hpp"
+#include "../runtime/backend.hpp"
 #include "../runtime/solver.hpp"
 
 using namespace heat3d;
@@ -62,6 +67,125 @@ static int run_reference_scheme(const Config& cfg) {
   return 0;
 }
 
+// One rank's run: banner, time loop, report (heat3D.cu:1078-1106), output.
+// Collective calls (run, compute_error, write_tecplot) are made by every rank.
+static int drive(const Config& cfg, Solver& solver) {
+  const bool root = solver.is_root();
+  if (root && !cfg.quiet) std::cout << cfg.echo_banner() << std::flush;
+  solver.initialize();
+  RunResult r = solver.run();
+  double gerr = 0, lerr = 0;
+  solver.compute_error(&gerr, &lerr);
+  if (root) {
+    std::printf("Computational time (parallel): %.6f\n\n", r.seconds);
+    if (r.converged)
+      std::printf("Simulation has converged in %lld iterations with a convergence threshold of %e\n",
+                  (long long)r.conv_iter, cfg.eps);
+    else
+      std::printf("Simulation did not converge within %lld iterations.\n", (long long)cfg.iter_max);
+    std::printf("L2-norm error: %.4f %%\n", 100.0 * (cfg.compat ? lerr : gerr));
+    if (!cfg.compat) {
+      const auto& d = solver.decomposition();
+      std::printf("heat3d: backend=%s comm=%s ranks=%d dims=%dx%dx%d dtype=%s kernel=%s "
+                  "iterations=%lld issued=%lld GLUPS=%.3f norm=%.6e last_residual=%.6e\n",
+                  solver.backend().name(), solver.comm().name(), solver.comm().size(),
+                  d.topo.dims[0], d.topo.dims[1], d.topo.dims[2], dtype_name(cfg.dtype),
+                  solver.kernel_name().c_str(), (long long)r.iterations, (long long)r.issued,
+                  r.glups, r.norm, r.last_residual);
+    }
+    if (cfg.timers) {
+      std::printf("heat3d: phase timing (ms/iteration, synchronised):");
+      for (auto& pt : solver.phase_times()) std::printf(" %s=%.4f", pt.first.c_str(), pt.second);
+      std::printf("\n");
+    }
+    if (r.fault) std::fprintf(stderr, "heat3d: non-finite residual detected at iteration %lld\n",
+                              (long long)r.conv_iter);
+    std::fflush(stdout);
+  }
+  // output/out.dat (heat3D.cu:1109-1179): on by default for small grids
+  std::string out = cfg.output;
+  const double pts = (double)cfg.n[0] * cfg.n[1] * cfg.n[2];
+  if (out == "auto") out = pts <= 2.2e6 ? "output/out.dat" : "none";
+  if (out != "none") solver.write_tecplot(out, cfg.tecplot_layout);
+  if (!cfg.json_out.empty() && root) {
+    io::Json j;
+    j.set_raw("N", "[" + std::to_string(cfg.n[0]) + ", " + std::to_string(cfg.n[1]) + ", " +
+                       std::to_string(cfg.n[2]) + "]");
+    j.set("dtype", std::string(dtype_name(cfg.dtype)));
+    j.set("backend", std::string(solver.backend().name()));
+    j.set("comm", std::string(solver.comm().name()));
+    j.set("ranks", (int64_t)solver.comm().size());
+    const auto& d = solver.decomposition();
+    j.set_raw("dims", "[" + std::to_string(d.topo.dims[0]) + ", " + std::to_string(d.topo.dims[1]) +
+                          ", " + std::to_string(d.topo.dims[2]) + "]");
+    j.set("kernel", solver.kernel_name());
+    j.set("eps", cfg.eps);
+    j.set("iter_max", (int64_t)cfg.iter_max);
+    j.set_bool("converged", r.converged);
+    j.set("conv_iter", (int64_t)r.conv_iter);
+    j.set("iterations", (int64_t)r.iterations);
+    j.set("issued", (int64_t)r.issued);
+    j.set("seconds", r.seconds);
+    j.set("glups", r.glups);
+    j.set("norm", r.norm);
+    j.set("last_residual", r.last_residual);
+    j.set("error_percent", 100.0 * gerr);
+    j.set("error_percent_rank0_local", 100.0 * lerr);
+    j.set_bool("fault", r.fault);
+    io::write_file_atomic(cfg.json_out, j.dump() + "\n");
+  }
+  return r.fault ? 3 : 0;
+}
+
+// --gpus N: one process, N ranks, one host thread per GPU (SURVEY.md L1 /
+// M1: the reference's MPI_Init replaced by ncclCommInitAll semantics: one
+// ncclUniqueId shared in memory, every thread calls ncclCommInitRank for its
+// device).  With --backend cpu the threads talk over loopback TCP sockets.
+static int run_threads(const Config& cfg) {
+  const int n = cfg.gpus;
+  BackendKind bk = cfg.backend;
+  if (bk == BackendKind::Auto) bk = hip_device_count() > 0 ? BackendKind::Hip : BackendKind::Cpu;
+  std::string uid;
+  if (bk == BackendKind::Hip) {
+    HEAT3D_CHECK(hip_device_count() >= n, "--gpus " << n << " but " << hip_device_count()
+                                                  << " GPU(s) visible (RCCL needs one device per rank)");
+    uid = rccl_unique_id();
+  }
+  const char* bp = std::getenv("HEAT3D_BOOTSTRAP_PORT");
+  const int port = bp && *bp ? std::atoi(bp) : 29501;
+  std::vector<int> codes(n, 2);
+  std::vector<std::thread> threads;
+  for (int r = 0; r < n; ++r) {
+    threads.emplace_back([&, r] {
+      try {
+        Config c = cfg;
+        c.backend = bk;
+        RankPlacement w;
+        w.rank = r;
+        w.size = n;
+        w.local_rank = r;
+        w.device = bk == BackendKind::Hip ? r : 0;
+        w.bootstrap_port = port;
+        w.rccl_uid = uid;
+        if (c.comm == CommKind::Auto) c.comm = bk == BackendKind::Hip ? CommKind::Rccl : CommKind::Socket;
+        if (bk == BackendKind::Cpu && c.cpu_threads == 0)
+          c.cpu_threads = std::max(1, (int)std::thread::hardware_concurrency() / n);
+        auto solver = make_solver(c, w);
+        codes[r] = drive(c, *solver);
+      } catch (const std::exception& e) {
+        // a failed rank would leave its peers blocked in collectives: end the job
+        std::cerr << "heat3d: rank " << r << " error: " << e.what() << std::endl;
+        std::fflush(stdout);
+        std::_Exit(2);
+      }
+    });
+  }
+  for (auto& t : threads) t.join();
+  int code = 0;
+  for (int c : codes) code = std::max(code, c);
+  return code;
+}
+
 int main(int argc, char** argv) {
   Config cfg;
   try {
@@ -76,72 +200,9 @@ int main(int argc, char** argv) {
   }
   try {
     if (cfg.scheme == "reference") return run_reference_scheme(cfg);
+    if (cfg.gpus > 1) return run_threads(cfg);
     auto solver = make_solver_from_env(cfg);
-    const bool root = solver->is_root();
-    if (root && !cfg.quiet) std::cout << cfg.echo_banner() << std::flush;
-    solver->initialize();
-    RunResult r = solver->run();
-    double gerr = 0, lerr = 0;
-    solver->compute_error(&gerr, &lerr);
-    if (root) {
-      std::printf("Computational time (parallel): %.6f\n\n", r.seconds);
-      if (r.converged)
-        std::printf("Simulation has converged in %lld iterations with a convergence threshold of %e\n",
-                    (long long)r.conv_iter, cfg.eps);
-      else
-        std::printf("Simulation did not converge within %lld iterations.\n", (long long)cfg.iter_max);
-      std::printf("L2-norm error: %.4f %%\n", 100.0 * (cfg.compat ? lerr : gerr));
-      if (!cfg.compat) {
-        const auto& d = solver->decomposition();
-        std::printf("heat3d: backend=%s comm=%s ranks=%d dims=%dx%dx%d dtype=%s kernel=%s "
-                    "iterations=%lld issued=%lld GLUPS=%.3f norm=%.6e last_residual=%.6e\n",
-                    solver->backend().name(), solver->comm().name(), solver->comm().size(),
-                    d.topo.dims[0], d.topo.dims[1], d.topo.dims[2], dtype_name(cfg.dtype),
-                    solver->kernel_name().c_str(), (long long)r.iterations, (long long)r.issued,
-                    r.glups, r.norm, r.last_residual);
-      }
-      if (cfg.timers) {
-        std::printf("heat3d: phase timing (ms/iteration, synchronised):");
-        for (auto& pt : solver->phase_times()) std::printf(" %s=%.4f", pt.first.c_str(), pt.second);
-        std::printf("\n");
-      }
-      if (r.fault) std::fprintf(stderr, "heat3d: non-finite residual detected at iteration %lld\n",
-                                (long long)r.conv_iter);
-      std::fflush(stdout);
-    }
-    // output/out.dat (heat3D.cu:1109-1179): on by default for small grids
-    std::string out = cfg.output;
-    const double pts = (double)cfg.n[0] * cfg.n[1] * cfg.n[2];
-    if (out == "auto") out = pts <= 2.2e6 ? "output/out.dat" : "none";
-    if (out != "none") solver->write_tecplot(out, cfg.tecplot_layout);
-    if (!cfg.json_out.empty() && root) {
-      io::Json j;
-      j.set_raw("N", "[" + std::to_string(cfg.n[0]) + ", " + std::to_string(cfg.n[1]) + ", " +
-                         std::to_string(cfg.n[2]) + "]");
-      j.set("dtype", std::string(dtype_name(cfg.dtype)));
-      j.set("backend", std::string(solver->backend().name()));
-      j.set("comm", std::string(solver->comm().name()));
-      j.set("ranks", (int64_t)solver->comm().size());
-      const auto& d = solver->decomposition();
-      j.set_raw("dims", "[" + std::to_string(d.topo.dims[0]) + ", " + std::to_string(d.topo.dims[1]) +
-                            ", " + std::to_string(d.topo.dims[2]) + "]");
-      j.set("kernel", solver->kernel_name());
-      j.set("eps", cfg.eps);
-      j.set("iter_max", (int64_t)cfg.iter_max);
-      j.set_bool("converged", r.converged);
-      j.set("conv_iter", (int64_t)r.conv_iter);
-      j.set("iterations", (int64_t)r.iterations);
-      j.set("issued", (int64_t)r.issued);
-      j.set("seconds", r.seconds);
-      j.set("glups", r.glups);
-      j.set("norm", r.norm);
-      j.set("last_residual", r.last_residual);
-      j.set("error_percent", 100.0 * gerr);
-      j.set("error_percent_rank0_local", 100.0 * lerr);
-      j.set_bool("fault", r.fault);
-      io::write_file_atomic(cfg.json_out, j.dump() + "\n");
-    }
-    return r.fault ? 3 : 0;
+    return drive(cfg, *solver);
   } catch (const std::exception& e) {
     std::cerr << "heat3d: error: " << e.what() << std::endl;
     return 2;

@@ -83,6 +83,8 @@ std::string Config::usage() {
      << "                            GPU runs, socket for multi-process CPU runs)\n"
      << "  --decomp AxBxC            process grid (default: balanced MPI_Dims_create split)\n"
      << "  --virtual-ranks P         P subdomains in one process (LocalComm)\n"
+     << "  --gpus N                  N ranks in this process, one host thread per GPU (RCCL; with\n"
+     << "                            --backend cpu: TCP sockets between the threads)\n"
      << "  --device N                GPU ordinal (default LOCAL_RANK)\n"
      << "  --graph / --no-graph      capture iterations in hipGraphs (default on)\n"
      << "  --no-overlap              do not split interior/boundary work\n"
@@ -90,7 +92,7 @@ std::string Config::usage() {
      << "  --kernel NAME             stencil kernel variant (auto|tile[:V:R:WZ:WY:L]|column|naive)\n"
      << "  --temporal 0|1|K          K-step temporal blocking, K = 2..6 (0 auto: on on the GPU for\n"
      << "                            one subdomain or x slabs; 1 off; results are bitwise identical)\n"
-     << "  --kernel2 tbK[:V:R:WZ:WY:L]  temporally blocked kernel variant (tb2, tbk2, tb3..tb6)\n"
+     << "  --kernel2 SPEC  temporally blocked kernel: tb2, tbk2, tb3..tb6 (queue), tr2..tr6 (register ring) [:V:R:WZ:WY:L:Q]\n"
      << "  --output PATH|none        Tecplot output (default output/out.dat for small grids)\n"
      << "  --tecplot-layout auto|ref|owned\n"
      << "  --compat                  reproduce reference reporting quirks\n"
@@ -167,6 +169,7 @@ Config Config::parse(int argc, const char* const* argv) {
       else throw UsageError("unknown comm '" + v + "'");
     } else if (key == "--decomp") c.decomp = parse_decomp(get("--decomp"));
     else if (key == "--virtual-ranks") c.virtual_ranks = (int)to_i64(get("--virtual-ranks"), "--virtual-ranks");
+    else if (key == "--gpus") c.gpus = (int)to_i64(get("--gpus"), "--gpus");
     else if (key == "--device") c.device = (int)to_i64(get("--device"), "--device");
     else if (key == "--graph") c.use_graph = true;
     else if (key == "--no-graph") c.use_graph = false;
@@ -213,6 +216,8 @@ Config Config::parse(int argc, const char* const* argv) {
     if (c.n[a] < 3) throw UsageError("each grid extent must be >= 3");
   if (c.iter_max < 0) throw UsageError("ITER_MAX must be >= 0");
   if (c.virtual_ranks < 1) throw UsageError("--virtual-ranks must be >= 1");
+  if (c.gpus < 0) throw UsageError("--gpus must be >= 1");
+  if (c.gpus > 1 && c.virtual_ranks > 1) throw UsageError("--gpus and --virtual-ranks are exclusive");
   if (c.check_every < 1) c.check_every = 1;
   if (c.graph_chunk < 2) c.graph_chunk = 2;
   if (c.graph_chunk % 2) c.graph_chunk += 1;

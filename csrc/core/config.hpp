@@ -44,6 +44,7 @@ struct Config {
   CommKind comm = CommKind::Auto;
   std::array<int, 3> decomp = {0, 0, 0};  // 0 = choose with dims_create
   int virtual_ranks = 1;                  // LocalComm: P subdomains in one process
+  int gpus = 0;                           // >1: this process runs that many ranks, one host thread per GPU
   int device = -1;                        // -1: LOCAL_RANK or 0
   bool use_graph = true;
   bool overlap = true;

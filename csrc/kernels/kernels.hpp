@@ -16,14 +16,18 @@
 namespace heat3d {
 
 struct KernelSpec {
-  enum Kind { Naive = 0, Column = 1, Tile = 2, TB2 = 3, TBK = 4 } kind = Tile;
-  int K = 0;  // TBK: time steps per sweep (TB2 is the tuned K = 2 kernel)
+  // TB2 / TBK / TBR advance K time steps per HBM sweep: TB2 is the tuned K = 2
+  // kernel (stencil_tb2.hip), TBK the queue kernel (stencil_tbk.hip), TBR the
+  // register-ring kernel (stencil_tbr.hip; its 7th field is the T^n ring size)
+  enum Kind { Naive = 0, Column = 1, Tile = 2, TB2 = 3, TBK = 4, TBR = 5 } kind = Tile;
+  int K = 0;  // multi-step kinds: time steps per sweep
   int WZ = 0, WY = 0;  // tile kernel: waves per workgroup along z and y
   int V = 0;  // elements per lane along z (0 = default for dtype)
   int R = 0;  // rows per wave along y (0 = default)
   int L = 0;  // x-segment length per wave (0 = auto)
   int O = -1; // tile order: 1 = z tiles fastest (default), 0 = y tiles fastest
   int NT = 0; // non-temporal output stores
+  bool multi_step() const { return kind == TB2 || kind == TBK || kind == TBR; }
   static KernelSpec parse(const std::string& s);
   std::string str() const;
   // zero (default) fields replaced by the tuned defaults for dtype t
@@ -74,6 +78,10 @@ void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream)
 void stencil2(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 // K-step temporally blocked sweep (stencil_tbk.hip), K = k.K
 void stencil_multi(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+// Same sweep, register-ring kernel (stencil_tbr.hip)
+void stencil_ring(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+// Any multi-step kind (TB2 / TBK / TBR) -> its kernel
+void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, void* stream);
 void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, void* stream);
 void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,

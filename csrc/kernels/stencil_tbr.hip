@@ -1,0 +1,407 @@
+// heat3d-mi355x — K-step temporally blocked FTCS kernel, register-ring form.
+//
+// Same algorithm and bitwise results as stencil_tbk.hip (one HBM sweep turns
+// T^n into T^{n+K}; stage s turns F_s = T^{n+s} into F_{s+1}, lagging stage
+// s-1 by one plane; every point goes through the reference update,
+// heat3D.cu:128-131, in the same expression order with contraction off), but
+// restructured after the rocprofv3 counters of stencil_tbk on MI355X
+// (profiles/pmc_tbk_vs_tbr.md): there, 28% of the wave cycles issued, 45%
+// waited, and of the VALU stream ~10% were plain register moves rotating
+// the x-queues, ~10% the NaN-propagating residual compares, and SALU work was
+// 40% of the VALU count.  Here
+//
+//   * queues are rings indexed by (step mod Q): the x-loop is unrolled by
+//     U = lcm(Q, 3) so every ring index is a compile-time constant and no
+//     value is ever moved between registers;
+//   * with Q = 4 the T^n plane x+2 is loaded at the start of step x (one full
+//     step of latency cover); with Q = 3 it is loaded into the slot stage 0
+//     has just freed (the remaining K-1 stages cover it) — fewer VGPRs;
+//   * the per-stage residual is a plain v_max_f64 (IEEE max, drops NaN) over
+//     the valid region; NaN detection moves to the stored T^{n+K}: a NaN
+//     produced at any stage at point p stays at p in every later stage (the
+//     centre term) and p is stored by exactly one tile, so if any stored
+//     value is NaN all K residual slots are set to NaN and the convergence
+//     check faults.  For NaN-free fields the residuals are bit-identical to
+//     the single-step kernels' (max of non-negative doubles is exact);
+//   * only WZ = 1 tiles (one wave spans the tile's z extent; the MI355X sweep
+//     showed z-split tiles lose), so z edges need no LDS.
+//
+// Tiles, Dirichlet ghosts, deep x halos and the u range are exactly as in
+// stencil_tbk.hip (shared TBKArgs geometry, launch_tbr mirrors launch_tbk).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "hip_helpers.hpp"
+
+namespace heat3d {
+namespace hip {
+
+struct TBRArgs {
+  int64_t sx, sy, origin;  // plane / row strides, element index of owned (0,0,0)
+  int blo[3], bhi[3];      // store box
+  int ulo, uhi;            // x range where F_{s+1} = FTCS(F_s)
+  int xlo_live, xhi_live;  // x planes present in memory
+  int kb0, yb0;            // first column / row of tile (0, 0)
+  int zstep, zring;        // tile stride along z, stored column ring
+  int nzb, nyb, seg;
+  int xq, xr;              // XCD remap: blocks per XCD (quotient / remainder)
+};
+
+namespace {
+
+constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
+constexpr int lcm_c(int a, int b) { return a / gcd_c(a, b) * b; }
+
+template <typename Real, int V>
+__device__ __forceinline__ void ldv(const Real* p, Real (&d)[V]) {
+  if constexpr (V == 1) {
+    d[0] = *p;
+  } else {
+    typedef typename VecOf<Real, V>::type Vec;
+    const Vec t = *reinterpret_cast<const Vec*>(p);
+#pragma unroll
+    for (int v = 0; v < V; ++v) d[v] = t[v];
+  }
+}
+
+template <typename Real, int V>
+__device__ __forceinline__ void stv(Real* p, const Real (&s)[V]) {
+  if constexpr (V == 1) {
+    *p = s[0];
+  } else {
+    typedef typename VecOf<Real, V>::type Vec;
+    Vec t;
+#pragma unroll
+    for (int v = 0; v < V; ++v) t[v] = s[v];
+    *reinterpret_cast<Vec*>(p) = t;
+  }
+}
+
+}  // namespace
+
+template <typename Real, int V, int R, int WY, int K, int Q>
+__global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ in,
+                                                       Real* __restrict__ out, TBRArgs g,
+                                                       Real Dx, Real Dy, Real Dz,
+                                                       unsigned long long* res,
+                                                       const int* done) {
+  static_assert(K >= 2 && K <= 6, "temporal depth");
+  static_assert(Q == 3 || Q == 4, "T^n ring size");
+  constexpr int TZ = 64 * V;
+  constexpr int TYB = WY * R;
+  constexpr int QS = 3;                 // stage ring: planes x-s-1, x-s, x-s+1
+  constexpr int U = lcm_c(Q, QS);       // x-loop unroll making ring indices static
+  static_assert(TYB > 2 * (K - 1) && R <= 32, "tile too small");
+  // centre-plane bottom/top rows of every stage, double-buffered by step parity
+  __shared__ __attribute__((aligned(16))) Real s_row[2][K][WY][2][TZ];
+  if (flag_set(done)) return;
+
+  const int blk = blockIdx.x;
+  const int xcd = blk & 7;
+  int t = xcd * g.xq + min(xcd, g.xr) + (blk >> 3);
+  const int zb = t % g.nzb;
+  t /= g.nzb;
+  const int ybk = t % g.nyb;
+  const int xs = t / g.nyb;
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int tkb = g.kb0 + zb * g.zstep;                 // tile's first column
+  const int tyb = g.yb0 + ybk * (TYB - 2 * (K - 1));    // tile's first row
+  const int k = tkb + lane * V;
+  const int yb = tyb + wave * R;
+  const int ylo = g.blo[1], yhi = g.bhi[1];
+  const int rlive = max(0, min(R, yhi + 1 - yb));  // rows <= yhi are loaded
+  const int xa = g.blo[0] + xs * g.seg;
+  const int xe = min(xa + g.seg, g.bhi[0]);
+  const int64_t sx = g.sx, sy = g.sy;
+
+  // per-lane column masks: in the box, stored, valid for the residual of stage s
+  bool zin[V], zst[V];
+  bool allst = true;
+  bool lres[K][V];  // stage s's residual counts this column
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int kk = k + v, cp = lane * V + v;
+    zin[v] = kk >= g.blo[2] && kk < g.bhi[2];
+    zst[v] = zin[v] && cp >= g.zring && cp < TZ - g.zring;
+    allst &= zst[v];
+#pragma unroll
+    for (int s = 0; s < K; ++s) lres[s][v] = zin[v] && cp >= s && cp < TZ - s;
+  }
+  const int64_t base0 = g.origin + (int64_t)yb * sy + k;
+  const int er = lane & 31;
+  const bool eload = er < rlive && yb + er >= -1;
+  const int64_t ebase = g.origin + (int64_t)(yb + er) * sy + (lane < 32 ? tkb - 1 : tkb + TZ);
+  const bool has_lo = wave > 0, has_hi = wave + 1 < WY;
+  const bool hb_live = !has_lo && yb - 1 >= -1 && rlive > 0;
+  const bool ht_live = !has_hi && yb + R <= yhi && rlive == R;
+
+  // rings: T^n plane p and its y/z halo live in slot (p - x0 + 1) mod Q;
+  // F_{s+1} produced at step x lives in f[s][(x - x0) mod 3]
+  Real q[Q][R][V];
+  Real hb[Q][V], ht[Q][V], ed[Q];
+  Real f[K - 1][QS][R][V];
+
+  auto plane_live = [&](int x) { return x >= g.xlo_live && x <= g.xhi_live; };
+  auto load_plane = [&](int x, Real (&d)[R][V], Real (&b)[V], Real (&tp)[V], Real& e) {
+    const bool pl = plane_live(x);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (pl && r < rlive && yb + r >= -1) {
+        ldv<Real, V>(in + base0 + (int64_t)x * sx + (int64_t)r * sy, d[r]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) d[r][v] = Real(0);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) b[v] = tp[v] = Real(0);
+    e = Real(0);
+    if (pl) {
+      if (hb_live) ldv<Real, V>(in + base0 + (int64_t)x * sx - sy, b);
+      if (ht_live) ldv<Real, V>(in + base0 + (int64_t)x * sx + (int64_t)R * sy, tp);
+      if (eload) e = in[ebase + (int64_t)x * sx];
+    }
+  };
+
+  const int x0 = xa - (K - 1);
+  const int xlast = xe + K - 2;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) load_plane(x0 - 1 + i, q[i], hb[i], ht[i], ed[i]);
+#pragma unroll
+  for (int s = 0; s < K - 1; ++s)
+#pragma unroll
+    for (int i = 0; i < QS; ++i)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int v = 0; v < V; ++v) f[s][i][r][v] = Real(0);
+
+  double m[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) m[s] = 0.0;
+  bool nan_seen = false;
+  int par = 0;
+
+  // whole chunks of U steps (no early exit: the unrolled body needs a constant
+  // trip count).  Steps past xlast only compute planes beyond the segment's
+  // widened box: nothing of them is stored or counted in a residual;
+  // launch_tbr sizes segments so that only a box's last segment pads.
+  for (int xb = x0; xb <= xlast; xb += U) {
+#pragma unroll
+    for (int ph = 0; ph < U; ++ph) {
+      const int x = xb + ph;
+      const int sM = ph % Q, sC = (ph + 1) % Q, sP = (ph + 2) % Q;
+      const int fw = ph % QS, fc = (ph + QS - 1) % QS, fm = (ph + QS - 2) % QS;
+      // T^n plane x+2 (Q = 4: its slot is free at the start of the step)
+      if constexpr (Q == 4) {
+        constexpr int sN = 3;
+        load_plane(x + 2, q[(ph + sN) % Q], hb[(ph + sN) % Q], ht[(ph + sN) % Q], ed[(ph + sN) % Q]);
+      }
+      // ---- publish the centre rows of every stage
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        Real (&C)[R][V] = s == 0 ? q[sC] : f[s > 0 ? s - 1 : 0][fc];
+        stv<Real, V>(&s_row[par][s][wave][0][lane * V], C[0]);
+        stv<Real, V>(&s_row[par][s][wave][1][lane * V], C[R - 1]);
+      }
+      __syncthreads();
+
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        Real (&M)[R][V] = s == 0 ? q[sM] : f[s > 0 ? s - 1 : 0][fm];
+        Real (&C)[R][V] = s == 0 ? q[sC] : f[s > 0 ? s - 1 : 0][fc];
+        Real (&P)[R][V] = s == 0 ? q[sP] : f[s > 0 ? s - 1 : 0][fw];
+        const int p = x - s;  // plane produced by this stage
+        const bool xin = p >= g.ulo && p < g.uhi;
+        const bool xval = x >= xa - K + 2 * s + 1;  // its inputs were valid
+        Real lo[V], hi[V];
+        if (has_lo) {
+          ldv<Real, V>(&s_row[par][s][wave - 1][1][lane * V], lo);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) lo[v] = s == 0 ? hb[sC][v] : C[0][v];
+        }
+        if (has_hi) {
+          ldv<Real, V>(&s_row[par][s][wave + 1][0][lane * V], hi);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) hi[v] = s == 0 ? ht[sC][v] : C[R - 1][v];
+        }
+        if (s < K - 1) {
+          Real (&N)[R][V] = f[s < K - 1 ? s : 0][fw];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int row = yb + r, rp = wave * R + r;
+            const bool yin = xin && row >= ylo && row < yhi;
+            // padded steps past xlast compute planes beyond the sweep's box
+            // widened by K-1-s (possibly from halo planes still being
+            // exchanged): never counted
+            const bool rres = yin && xval && x <= xlast && rp >= s && rp < TYB - s;
+            const Real left = s == 0 ? readlane(ed[sC], r) : C[r][0];
+            const Real right = s == 0 ? readlane(ed[sC], 32 + r) : C[r][V - 1];
+            const Real* ym = r == 0 ? lo : C[r > 0 ? r - 1 : 0];
+            const Real* yp = r == R - 1 ? hi : C[r + 1 < R ? r + 1 : 0];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+              const Real zm = v == 0 ? dpp_shr1(left, C[r][V - 1]) : C[r][v > 0 ? v - 1 : 0];
+              const Real zp = v == V - 1 ? dpp_shl1(right, C[r][0]) : C[r][v + 1 < V ? v + 1 : 0];
+              const Real nv = ftcs<Real>(C[r][v], M[r][v], P[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
+              N[r][v] = (yin && zin[v]) ? nv : C[r][v];
+              if (rres) m[s] = fmax(m[s], lres[s][v] ? fabs((double)nv - (double)C[r][v]) : 0.0);
+            }
+          }
+        } else {
+          // final stage: T^{n+K}(p) on the stored region
+          if (p >= xa && p < xe) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const int row = yb + r, rp = wave * R + r;
+              const bool rst = row >= ylo && row < yhi && rp >= K - 1 && rp < TYB - (K - 1);
+              if (!rst) continue;
+              const Real* ym = r == 0 ? lo : C[r > 0 ? r - 1 : 0];
+              const Real* yp = r == R - 1 ? hi : C[r + 1 < R ? r + 1 : 0];
+              Real nv[V];
+#pragma unroll
+              for (int v = 0; v < V; ++v) {
+                const Real zm = v == 0 ? dpp_shr1(C[r][0], C[r][V - 1]) : C[r][v > 0 ? v - 1 : 0];
+                const Real zp = v == V - 1 ? dpp_shl1(C[r][V - 1], C[r][0]) : C[r][v + 1 < V ? v + 1 : 0];
+                nv[v] = ftcs<Real>(C[r][v], M[r][v], P[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
+                const double d = fabs((double)nv[v] - (double)C[r][v]);
+                m[s] = fmax(m[s], zst[v] ? d : 0.0);
+                nan_seen |= zst[v] && nv[v] != nv[v];
+              }
+              Real* dst = out + base0 + (int64_t)p * sx + (int64_t)r * sy;
+              if (allst) {
+                stv<Real, V>(dst, nv);
+              } else {
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                  if (zst[v]) dst[v] = nv[v];
+              }
+            }
+          }
+        }
+        // T^n plane x+2 into the slot stage 0 has just freed (Q = 3)
+        if constexpr (Q == 3) {
+          if (s == 0) load_plane(x + 2, q[sM], hb[sM], ht[sM], ed[sM]);
+        }
+      }
+      par ^= 1;
+    }
+  }
+  if (res) {
+    if (__any(nan_seen)) {
+      if (lane == 0)
+#pragma unroll
+        for (int s = 0; s < K; ++s) atomicMax(res + s, 0x7ff8000000000000ULL);
+    }
+#pragma unroll
+    for (int s = 0; s < K; ++s) residual_commit(res + s, m[s]);
+  }
+}
+
+template <typename Real, int V, int R, int WY, int K, int Q>
+static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
+  const Box& b = p.box;
+  constexpr int TZ = 64 * V;
+  constexpr int TYB = WY * R;
+  const Layout& L = p.L;
+  HEAT3D_CHECK(L.gx >= 1 && L.n[0] + 2 * L.gx < (1LL << 30) && L.n[1] + 2 < (1LL << 30) &&
+                   L.sy < (1LL << 30),
+               "tbr: extents exceed 32-bit tile coordinates");
+  TBRArgs g;
+  g.sx = L.sx;
+  g.sy = L.sy;
+  g.origin = L.origin;
+  for (int a = 0; a < 3; ++a) {
+    g.blo[a] = (int)b.lo[a];
+    g.bhi[a] = (int)b.hi[a];
+  }
+  g.ulo = (int)(p.ux[1] >= p.ux[0] ? p.ux[0] : b.lo[0]);
+  g.uhi = (int)(p.ux[1] >= p.ux[0] ? p.ux[1] : b.hi[0]);
+  g.xlo_live = (int)-L.gx;
+  g.xhi_live = (int)(L.n[0] + L.gx - 1);
+  HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live && g.ulo <= b.lo[0] &&
+                   g.uhi >= b.hi[0],
+               "tbr: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
+  g.zring = ((K - 1 + V - 1) / V) * V;
+  g.zstep = TZ - 2 * g.zring;
+  HEAT3D_CHECK(g.zstep > 0, "tbr: tile too narrow for depth " << K);
+  int64_t kb0 = b.lo[2] - g.zring;
+  kb0 = (kb0 >= 0 ? kb0 / V : -((-kb0 + V - 1) / V)) * V;  // floor to a multiple of V
+  g.kb0 = (int)kb0;
+  g.yb0 = (int)(b.lo[1] - (K - 1));
+  const int64_t zspan = b.hi[2] - (kb0 + g.zring);
+  g.nzb = (int)std::max<int64_t>(1, (zspan + g.zstep - 1) / g.zstep);
+  const int ystep = TYB - 2 * (K - 1);
+  g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + ystep - 1) / ystep);
+  int seg = ks.L;
+  if (seg <= 0) {
+    static int slots = 0;
+    if (!slots)
+      slots = device_slots(reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q>), 64 * WY);
+    seg = choose_segment(b.extent(0), (int64_t)g.nzb * g.nyb, slots, 2 * K);
+    // a segment runs seg + 2(K-1) steps in chunks of U = lcm(Q, 3)
+    constexpr int U = Q == 3 ? 3 : 12;
+    const int steps = seg + 2 * (K - 1);
+    seg += (U - steps % U) % U;
+  }
+  g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));
+  const int64_t nxs = (b.extent(0) + g.seg - 1) / g.seg;
+  const int64_t nblocks = (int64_t)g.nzb * g.nyb * nxs;
+  HEAT3D_CHECK(nblocks < (1LL << 31), "too many blocks");
+  g.xq = (int)(nblocks / 8);
+  g.xr = (int)(nblocks % 8);
+  HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tbr: residual slots " << p.slot << "+" << K);
+  unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
+  const int* done = p.state ? &p.state->done : nullptr;
+  hipLaunchKernelGGL((stencil_tbr<Real, V, R, WY, K, Q>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+                     static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0],
+                     (Real)p.D[1], (Real)p.D[2], r, done);
+  HIPK_CHECK(hipGetLastError());
+}
+
+template <typename Real>
+static void dispatch_tbr(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
+  const int K = k.K;
+  const KernelSpec r = k.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
+  const int V = r.V, R = r.R, WY = r.WY, Q = r.NT;
+  HEAT3D_CHECK(r.WZ == 1, "tbr kernels span the tile's z extent with one wave (WZ = 1)");
+#define H3D_TBR(VV, RR, YY, KK, QQ)                            \
+  if (V == VV && R == RR && WY == YY && K == KK && Q == QQ) {  \
+    launch_tbr<Real, VV, RR, YY, KK, QQ>(p, k, s);             \
+    return;                                                    \
+  }
+#define H3D_TBR_Q(VV, RR, YY, KK) H3D_TBR(VV, RR, YY, KK, 3) H3D_TBR(VV, RR, YY, KK, 4)
+  H3D_TBR_Q(1, 4, 16, 2) H3D_TBR_Q(1, 4, 16, 3) H3D_TBR_Q(1, 4, 16, 4)
+  H3D_TBR_Q(1, 4, 8, 3) H3D_TBR_Q(1, 4, 8, 4) H3D_TBR_Q(1, 6, 8, 3) H3D_TBR_Q(1, 3, 16, 3)
+  H3D_TBR_Q(1, 2, 16, 2) H3D_TBR_Q(2, 2, 8, 2) H3D_TBR_Q(2, 2, 16, 2)
+  if constexpr (sizeof(Real) == 4) {
+    H3D_TBR_Q(2, 4, 8, 3) H3D_TBR_Q(2, 4, 8, 4) H3D_TBR_Q(2, 4, 16, 3) H3D_TBR_Q(2, 4, 8, 2)
+  }
+#undef H3D_TBR_Q
+#undef H3D_TBR
+  HEAT3D_THROW("unsupported tbr kernel variant V=" << V << " R=" << R << " WY=" << WY << " K=" << K
+                                                   << " Q=" << Q);
+}
+
+void stencil_ring(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
+  if (p.box.empty()) return;
+  if (t == DType::F64) dispatch_tbr<double>(p, k, S(stream));
+  else dispatch_tbr<float>(p, k, S(stream));
+}
+
+void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
+  switch (k.kind) {
+    case KernelSpec::TBR: stencil_ring(t, p, k, stream); break;
+    case KernelSpec::TBK: stencil_multi(t, p, k, stream); break;
+    case KernelSpec::TB2: stencil2(t, p, k, stream); break;
+    default: HEAT3D_THROW("sweep needs a multi-step kernel (tb2 | tbk2 | tb3..tb6 | tr2..tr6)");
+  }
+}
+
+}  // namespace hip
+}  // namespace heat3d

@@ -243,12 +243,8 @@ PYBIND11_MODULE(_heat3d, m) {
     std::array<int64_t, 6> box = {0, n[0], 0, n[1], 0, n[2]};
     auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
     KernelSpec k = KernelSpec::parse(kernel);
-    if (k.kind == KernelSpec::TBK) {
-      hip::stencil_multi(t, p, k, reinterpret_cast<void*>(stream));
-    } else {
-      k.kind = KernelSpec::TB2;
-      hip::stencil2(t, p, k, reinterpret_cast<void*>(stream));
-    }
+    if (!k.multi_step()) k.kind = KernelSpec::TB2;
+    hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
   });
   // multi-step sweep on a sub-box of a layout with gx ghost planes, u range ux
   // (the solver's slab path); kernel = tb2 / tbk2 / tb3..tb6 spec
@@ -262,9 +258,8 @@ PYBIND11_MODULE(_heat3d, m) {
     p.ux[0] = ux[0];
     p.ux[1] = ux[1];
     KernelSpec k = KernelSpec::parse(kernel);
-    if (k.kind == KernelSpec::TBK) hip::stencil_multi(t, p, k, reinterpret_cast<void*>(stream));
-    else if (k.kind == KernelSpec::TB2) hip::stencil2(t, p, k, reinterpret_cast<void*>(stream));
-    else throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 kernel");
+    if (!k.multi_step()) throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 / tr2..tr6 kernel");
+    hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
   });
   hk.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
                           std::array<int64_t, 3> N, std::array<double, 3> h, int64_t stream) {
@@ -316,8 +311,7 @@ PYBIND11_MODULE(_heat3d, m) {
     p.ux[0] = ux[0];
     p.ux[1] = ux[1];
     KernelSpec k = KernelSpec::parse(kernel);
-    if (k.kind != KernelSpec::TB2 && k.kind != KernelSpec::TBK)
-      throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 kernel");
+    if (!k.multi_step()) throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 / tr2..tr6 kernel");
     std::vector<char> s0(p.L.bytes()), s1(p.L.bytes());
     py::gil_scoped_release nogil;
     cpu::stencil_multi(t, p, k.K, k.kind == KernelSpec::TB2, s0.data(), s1.data());

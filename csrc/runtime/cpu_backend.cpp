@@ -57,14 +57,14 @@ class CpuBackend final : public Backend {
   // (tb2: slots slot, slot ^ 1).
   void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId) override {
     if (p.state && p.state->done) return;
-    const int K = k.kind == KernelSpec::TBK ? k.K : 2;
+    const int K = k.kind == KernelSpec::TB2 ? 2 : k.K;
     for (int i = 0; i < 2; ++i)
       if (scratch_bytes_[i] < p.L.bytes()) {
         release(scratch_[i]);
         scratch_[i] = alloc(p.L.bytes());
         scratch_bytes_[i] = p.L.bytes();
       }
-    cpu::stencil_multi(t, p, K, k.kind != KernelSpec::TBK, scratch_[0], scratch_[1]);
+    cpu::stencil_multi(t, p, K, k.kind == KernelSpec::TB2, scratch_[0], scratch_[1]);
   }
   ~CpuBackend() override {
     release(scratch_[0]);

@@ -159,8 +159,7 @@ class HipBackend final : public Backend {
     hip::stencil(t, p, k, streams_[s]);
   }
   void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) override {
-    if (k.kind == KernelSpec::TBK) hip::stencil_multi(t, p, k, streams_[s]);
-    else hip::stencil2(t, p, k, streams_[s]);
+    hip::sweep(t, p, k, streams_[s]);
   }
   void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, StreamId s) override {
     hip::pack_box(t, f, L, b, buf, streams_[s]);

@@ -36,11 +36,15 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     if (parts.size() > 5) k.NT = std::atoi(parts[5].c_str());
   } else if (parts[0] == "tile" || parts[0] == "tb2" || parts[0] == "tbk2" ||
              (parts[0].size() == 3 && parts[0][0] == 't' && parts[0][1] == 'b' && parts[0][2] >= '3' &&
+              parts[0][2] <= '6') ||
+             (parts[0].size() == 3 && parts[0][0] == 't' && parts[0][1] == 'r' && parts[0][2] >= '2' &&
               parts[0][2] <= '6')) {
-    // tile = single step; tb2 = tuned 2-step kernel; tb3..tb6 / tbk2 = K-step kernel
-    k.kind = parts[0] == "tile" ? Tile : parts[0] == "tb2" ? TB2 : TBK;
+    // tile = single step; tb2 = tuned 2-step kernel; tb3..tb6 / tbk2 = K-step
+    // queue kernel; tr2..tr6 = K-step register-ring kernel
+    k.kind = parts[0] == "tile" ? Tile : parts[0] == "tb2" ? TB2 : parts[0][1] == 'r' ? TBR : TBK;
     if (k.kind == TB2) k.K = 2;
     if (k.kind == TBK) k.K = parts[0] == "tbk2" ? 2 : parts[0][2] - '0';
+    if (k.kind == TBR) k.K = parts[0][2] - '0';
     auto at = [&](std::size_t i) { return parts.size() > i ? std::atoi(parts[i].c_str()) : 0; };
     k.V = at(1);
     k.R = at(2);
@@ -85,6 +89,13 @@ KernelSpec KernelSpec::resolved(DType t) const {
       def(r.WY, f64 ? 16 : 8);
       def(r.NT, 1);  // prefetch depth
       break;
+    case TBR:  // same tiles as TBK; 7th field = T^n ring size (4: full-step prefetch)
+      def(r.V, f64 ? 1 : 2);
+      def(r.R, 4);
+      def(r.WZ, 1);
+      def(r.WY, f64 ? 16 : 8);
+      def(r.NT, 4);
+      break;
     default:
       break;
   }
@@ -93,10 +104,14 @@ KernelSpec KernelSpec::resolved(DType t) const {
 
 std::string KernelSpec::str() const {
   if (kind == Naive) return "naive";
-  if (kind == Tile || kind == TB2 || kind == TBK) {
+  if (kind == Tile || multi_step()) {
     std::ostringstream os;
-    os << (kind == Tile ? "tile:" : kind == TB2 ? "tb2:" : K == 2 ? "tbk2:" : "tb" + std::to_string(K) + ":") << V << ":" << R << ":" << WZ << ":" << WY << ":" << L
-       << ":" << NT;
+    os << (kind == Tile  ? std::string("tile:")
+           : kind == TB2 ? std::string("tb2:")
+           : kind == TBR ? "tr" + std::to_string(K) + ":"
+           : K == 2      ? std::string("tbk2:")
+                         : "tb" + std::to_string(K) + ":")
+       << V << ":" << R << ":" << WZ << ":" << WY << ":" << L << ":" << NT;
     return os.str();
   }
   std::ostringstream os;
@@ -132,10 +147,12 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   // Auto depth: 3 for one subdomain; 2 for x slabs, whose K-plane boundary
   // slabs cost more than the saved traffic at K = 3 (profiles/kernel_sweep.md)
   int K = cfg_.temporal >= 2 ? cfg_.temporal
-          : (kspec2_.kind == KernelSpec::TB2 || kspec2_.kind == KernelSpec::TBK) ? kspec2_.K
+          : kspec2_.multi_step() ? kspec2_.K
           : dims[0] > 1 ? 2
                         : kDefaultTemporal;
-  if (K == 2 && kspec2_.kind != KernelSpec::TBK) {
+  if (kspec2_.kind == KernelSpec::TBR) {
+    // explicitly requested register-ring kernel: any depth
+  } else if (K == 2 && kspec2_.kind != KernelSpec::TBK) {
     kspec2_.kind = KernelSpec::TB2;
   } else {
     kspec2_.kind = KernelSpec::TBK;
@@ -1165,14 +1182,23 @@ static int env_int(const char* a, const char* b, int dflt) {
 }
 
 std::unique_ptr<Solver> make_solver_from_env(const Config& cfg) {
-  const int rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", env_int("PMI_RANK", nullptr, 0));
-  const int size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", env_int("PMI_SIZE", nullptr, 1));
-  const int local_rank = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", env_int("MPI_LOCALRANKID", nullptr, rank));
+  RankPlacement w;
+  w.rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", env_int("PMI_RANK", nullptr, 0));
+  w.size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", env_int("PMI_SIZE", nullptr, 1));
+  w.local_rank = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", env_int("MPI_LOCALRANKID", nullptr, w.rank));
   const char* ma = std::getenv("MASTER_ADDR");
-  const std::string master = ma && *ma ? ma : "127.0.0.1";
+  w.master = ma && *ma ? ma : "127.0.0.1";
   // The native CLI never shares a process with torch, but torchrun's agent owns
   // MASTER_PORT; bootstrap on MASTER_PORT + 1 unless told otherwise.
-  const int bport = env_int("HEAT3D_BOOTSTRAP_PORT", nullptr, env_int("MASTER_PORT", nullptr, 29500) + 1);
+  w.bootstrap_port = env_int("HEAT3D_BOOTSTRAP_PORT", nullptr, env_int("MASTER_PORT", nullptr, 29500) + 1);
+  w.device = cfg.device;
+  return make_solver(cfg, w);
+}
+
+std::unique_ptr<Solver> make_solver(const Config& cfg, const RankPlacement& w) {
+  const int rank = w.rank, size = w.size, local_rank = w.local_rank;
+  const std::string& master = w.master;
+  const int bport = w.bootstrap_port;
 
   BackendKind bk = cfg.backend;
   if (bk == BackendKind::Auto) bk = hip_device_count() > 0 ? BackendKind::Hip : BackendKind::Cpu;
@@ -1182,8 +1208,8 @@ std::unique_ptr<Solver> make_solver_from_env(const Config& cfg) {
     else if (size > 1) ck = bk == BackendKind::Hip ? CommKind::Rccl : CommKind::Socket;
     else ck = CommKind::None;
   }
-  int device = cfg.device >= 0 ? cfg.device : 0;
-  if (bk == BackendKind::Hip && cfg.device < 0) {
+  int device = w.device >= 0 ? w.device : 0;
+  if (bk == BackendKind::Hip && w.device < 0) {
     const int n = hip_device_count();
     device = n > 0 ? local_rank % n : 0;
   }
@@ -1210,10 +1236,14 @@ std::unique_ptr<Solver> make_solver_from_env(const Config& cfg) {
     }
     case CommKind::Rccl: {
       HEAT3D_CHECK(bk == BackendKind::Hip, "RCCL needs the HIP backend");
-      net::Bootstrap boot(rank, size, master, bport);
-      std::string uid = rank == 0 ? rccl_unique_id() : std::string();
-      auto all = boot.allgather(uid);
-      comm = make_rccl_comm(rank, size, all[0], device);
+      if (!w.rccl_uid.empty()) {
+        comm = make_rccl_comm(rank, size, w.rccl_uid, device);
+      } else {
+        net::Bootstrap boot(rank, size, master, bport);
+        std::string uid = rank == 0 ? rccl_unique_id() : std::string();
+        auto all = boot.allgather(uid);
+        comm = make_rccl_comm(rank, size, all[0], device);
+      }
       nranks = size;
       break;
     }

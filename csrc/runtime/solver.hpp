@@ -230,10 +230,25 @@ class Solver {
   void accumulate_phase_times();
 };
 
-// Build a Solver for a parsed command line in this process: chooses backend,
-// comm (RCCL / socket via env bootstrap, LocalComm for --virtual-ranks),
-// decomposition.  Environment: RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/
-// MASTER_PORT (torchrun / mpirun style).
+// Where one rank of a job runs: its rank, the job size, the GPU it binds, and
+// how it meets its peers (rank 0's bootstrap address / port).  With a
+// non-empty rccl_uid the RCCL communicator is created directly from it (the
+// ranks of one process share it: ncclCommInitAll semantics, one host thread
+// per GPU) instead of through the TCP bootstrap.
+struct RankPlacement {
+  int rank = 0, size = 1, local_rank = 0;
+  int device = -1;  // -1: local_rank modulo the visible devices
+  std::string master = "127.0.0.1";
+  int bootstrap_port = 29501;
+  std::string rccl_uid;
+};
+
+// Build a Solver for one rank: chooses backend, comm (RCCL / socket through
+// the bootstrap, LocalComm for --virtual-ranks), decomposition.
+std::unique_ptr<Solver> make_solver(const Config& cfg, const RankPlacement& where);
+
+// Same, placement from the environment: RANK/WORLD_SIZE/LOCAL_RANK/
+// MASTER_ADDR/MASTER_PORT (torchrun / mpirun style).
 std::unique_ptr<Solver> make_solver_from_env(const Config& cfg);
 
 }  // namespace heat3d

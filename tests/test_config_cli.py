@@ -110,3 +110,31 @@ def test_cli_multiprocess_socket(heat3d_bin, tmp_path):
     assert outs[1][0] == ""  # only rank 0 reports
     zones = (tmp_path / "output" / "out.dat").read_text().count("ZONE")
     assert zones == 2
+
+
+@pytest.mark.parametrize("gpus,decomp", [(2, None), (4, "1x2x2"), (3, None)])
+def test_threads_per_rank_cli(heat3d_bin, tmp_path, gpus, decomp):
+    """--gpus N: N ranks in one process, one host thread each (the
+    ncclCommInitAll-style runtime; TCP sockets between the threads on the CPU
+    backend).  Same report and checkpoint as the single-rank run."""
+    base = ["23", "23", "23", "100000", "1e-4", "--backend", "cpu", "--output", "none"]
+    one = run_cli(base + ["--checkpoint-every", "64", "--checkpoint-dir", "c1", "--json-out", "a.json"], tmp_path)
+    assert one.returncode == 0, one.stderr
+    args = base + ["--gpus", str(gpus), "--checkpoint-every", "64", "--checkpoint-dir", "cn", "--json-out", "b.json"]
+    if decomp:
+        args += ["--decomp", decomp]
+    many = run_cli(args, tmp_path, env={"HEAT3D_BOOTSTRAP_PORT": str(free_port())})
+    assert many.returncode == 0, many.stderr
+    a = json.loads((tmp_path / "a.json").read_text())
+    b = json.loads((tmp_path / "b.json").read_text())
+    assert b["ranks"] == gpus and b["comm"] == "socket"
+    assert a["conv_iter"] == b["conv_iter"] and abs(a["error_percent"] - b["error_percent"]) < 1e-12
+    assert many.stdout.count("Runnung HeatEquation3D") == 1  # one report per job, not per thread
+    ra = np.fromfile(tmp_path / "c1" / "field.raw", dtype=np.float64)
+    rb = np.fromfile(tmp_path / "cn" / "field.raw", dtype=np.float64)
+    assert np.array_equal(ra, rb)
+
+
+def test_threads_per_rank_needs_devices(heat3d_bin, tmp_path):
+    r = run_cli(["23", "23", "23", "10", "1e-4", "--backend", "hip", "--gpus", "64"], tmp_path)
+    assert r.returncode != 0

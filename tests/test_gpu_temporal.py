@@ -103,9 +103,12 @@ def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
     assert np.array_equal(a.gather(), b.gather())
 
 
-VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb3:1:4:1:16", "tb3:1:6:1:8", "tb3:1:4:2:8", "tb3:1:4:1:8:3"],
-              4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1"],
-              2: ["tbk2", "tbk2:2:2:1:8"]}
+VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb3:1:4:1:16", "tb3:1:6:1:8", "tb3:1:4:2:8", "tb3:1:4:1:8:3",
+                  "tr3", "tr3:1:4:1:16:0:3", "tr3:1:3:1:16:0:3", "tr3:1:4:1:8:0:4", "tr3:1:6:1:8:0:3", "tr3:1:4:1:8:5:3"],
+              4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1", "tr4", "tr4:1:4:1:8:0:3"],
+              2: ["tbk2", "tbk2:2:2:1:8", "tr2", "tr2:2:2:1:8:0:3", "tr2:1:4:1:16:0:3", "tr2:2:2:1:16"]}
+VARIANTS_K_F32 = {3: ["tr3:2:4:1:8:0:3", "tr3:2:4:1:8:0:4", "tr3:2:4:1:16:0:4"], 4: ["tr4:2:4:1:8:0:4"],
+                  2: ["tr2:2:4:1:8:0:3", "tr2:2:4:1:8:0:4"]}
 
 
 @pytest.mark.parametrize("K", [2, 3, 4])
@@ -123,7 +126,7 @@ def test_stencil_k_bitwise(h3d, gpu, K, dtype, n):
         T[1:-1, 1:-1, 1:-1] = u
         refs.append(r)
     want = T[1:-1, 1:-1, 1:-1]
-    for v in VARIANTS_K[K]:
+    for v in VARIANTS_K[K] + (VARIANTS_K_F32[K] if dtype == torch.float32 else []):
         out = ops.PaddedField(n, dtype=dtype, device=gpu)
         out.flat.fill_(-3.0)
         st = ops.new_state(gpu)
@@ -163,7 +166,8 @@ def _deep_random(ops, n, gx, dtype, seed):
     return f
 
 
-@pytest.mark.parametrize("kernel", ["tb2", "tbk2", "tb3", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb4", "tb4:1:6:1:8"])
+@pytest.mark.parametrize("kernel", ["tb2", "tbk2", "tb3", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb4", "tb4:1:6:1:8",
+                                    "tr2", "tr3", "tr3:1:4:1:16:0:3", "tr4", "tr2:2:2:1:8:0:3"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (5, (0, 5), "lo"), (9, (0, 9), "hi"),
                                             (12, (4, 8), "both"), (12, (0, 4), "both"), (12, (8, 12), "both"),
@@ -213,3 +217,31 @@ def test_temporal_mixed_steps_gpu(h3d, gpu, K, vr):
     a.synchronize()
     assert a.state()["iter"] == b.state()["iter"] == 194
     assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("kernel2", ["tr3", "tr3:1:4:1:16:0:3", "tr2", "tr4"])
+@pytest.mark.parametrize("vr", [1, 3])
+def test_ring_kernel_solver_gpu(h3d, gpu, kernel2, vr):
+    """Register-ring sweeps (stencil_tbr.hip) in the solver, single domain and
+    x slabs: bitwise equal to the CPU single-step solver, same convergence."""
+    n = (67, 45, 131)
+    a = h3d.HeatSolver(n, 10 ** 6, 1e-4, backend="hip", virtual_ranks=vr, decomp=(vr, 1, 1),
+                       extra_args=["--kernel2", kernel2])
+    assert a.native.temporal_blocking and a.kernel.startswith(kernel2.split(":")[0]), a.kernel
+    b = h3d.HeatSolver(n, 10 ** 6, 1e-4, backend="cpu", extra_args=["--temporal", "1"])
+    ra, rb = a.run(), b.run()
+    assert ra["conv_iter"] == rb["conv_iter"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("kernel2", ["tr3", "tr2", "tb3", "tb2"])
+def test_sweep_nan_faults(h3d, gpu, kernel2):
+    """A NaN anywhere in the field reaches the convergence check as a fault
+    (the ring kernel detects it on the stored T^{n+K} and poisons every slot)."""
+    s = h3d.HeatSolver((41, 37, 45), 10 ** 6, 1e-5, backend="hip", extra_args=["--kernel2", kernel2])
+    s.initialize()
+    s.step(12)
+    s.synchronize()
+    s.native.inject(0, 20, 18, 22, float("nan"))
+    r = s.run()
+    assert r["fault"] and not r["converged"], r
