@@ -46,6 +46,7 @@ def main() -> int:
     ap.add_argument("--converge-eps", type=float, default=1e-3,
                     help="also measure time-to-converge at this EPS (0 disables)")
     ap.add_argument("--temporal", type=int, default=0, help="0 auto | 1 single-step | K (2..6) K-step temporally blocked sweeps")
+    ap.add_argument("--kernel2", default="auto", help="temporally blocked sweep kernel (tbK / trK[:V:R:WZ:WY:L:Q])")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: split the grid into this many subdomains on one GPU (not the headline)")
     ap.add_argument("--json-out", default="")
@@ -93,7 +94,7 @@ def main() -> int:
                           decomp=dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
                           device=dev, group=group, virtual_ranks=args.virtual_ranks,
-                          extra_args=["--temporal", str(args.temporal)])
+                          extra_args=["--temporal", str(args.temporal), "--kernel2", args.kernel2])
 
     s = make(0.0, 1 << 40)
     s.initialize()

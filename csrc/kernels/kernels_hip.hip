@@ -643,15 +643,18 @@ void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* d
 }
 
 // ---- convergence check (single lane) ------------------------------------------
-__global__ void check_kernel(DeviceState* s, int slot) {
+__global__ void check_kernel(DeviceState* s, int slot, int count) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const double r = __builtin_bit_cast(double, (long long)s->residual[slot]);
-  check_convergence_scalar(s, r);
-  s->residual[slot] = kResidualInitBits;
+  for (int i = slot; i < slot + count; ++i) {
+    const double r = __builtin_bit_cast(double, (long long)s->residual[i]);
+    check_convergence_scalar(s, r);
+    s->residual[i] = kResidualInitBits;
+  }
 }
 
-void check_convergence(DeviceState* s, int slot, void* stream) {
-  hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, S(stream), s, slot);
+void check_convergence(DeviceState* s, int slot, void* stream, int count) {
+  HEAT3D_CHECK(slot >= 0 && count >= 1 && slot + count <= kResidualSlots, "residual slots " << slot << "+" << count);
+  hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, S(stream), s, slot, count);
   HIPK_CHECK(hipGetLastError());
 }
 

@@ -5,7 +5,7 @@
 // s-1 by one plane; every point goes through the reference update,
 // heat3D.cu:128-131, in the same expression order with contraction off), but
 // restructured after the rocprofv3 counters of stencil_tbk on MI355X
-// (profiles/pmc_tbk_vs_tbr.md): there, 28% of the wave cycles issued, 45%
+// (profiles/pmc_tbk.md, profiles/kernel_sweep.md): there, 28% of the wave cycles issued, 45%
 // waited, and of the VALU stream ~10% were plain register moves rotating
 // the x-queues, ~10% the NaN-propagating residual compares, and SALU work was
 // 40% of the VALU count.  Here
@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "hip_helpers.hpp"
 
@@ -105,7 +106,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   const int ybk = t % g.nyb;
   const int xs = t / g.nyb;
 
-  const int wave = threadIdx.x >> 6;
+  // the wave index is uniform: keep it (and every row / plane offset derived
+  // from it) in SGPRs, so that a load is an SGPR base + one shared VGPR lane
+  // offset instead of a 64-bit VGPR address per row and step
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int tkb = g.kb0 + zb * g.zstep;                 // tile's first column
   const int tyb = g.yb0 + ybk * (TYB - 2 * (K - 1));    // tile's first row
@@ -130,10 +134,14 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
 #pragma unroll
     for (int s = 0; s < K; ++s) lres[s][v] = zin[v] && cp >= s && cp < TZ - s;
   }
-  const int64_t base0 = g.origin + (int64_t)yb * sy + k;
+  // uniform element offset of (plane 0, row yb, column tkb); lanes add lane * V
+  const int64_t wbase = g.origin + (int64_t)yb * sy + tkb;
+  const Real* __restrict__ inw = in + wbase;
+  Real* __restrict__ outw = out + wbase;
+  const int lo_off = lane * V;
   const int er = lane & 31;
   const bool eload = er < rlive && yb + er >= -1;
-  const int64_t ebase = g.origin + (int64_t)(yb + er) * sy + (lane < 32 ? tkb - 1 : tkb + TZ);
+  const int eoff = er * (int)sy + (lane < 32 ? -1 : TZ);  // halo column of row er
   const bool has_lo = wave > 0, has_hi = wave + 1 < WY;
   const bool hb_live = !has_lo && yb - 1 >= -1 && rlive > 0;
   const bool ht_live = !has_hi && yb + R <= yhi && rlive == R;
@@ -150,7 +158,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (pl && r < rlive && yb + r >= -1) {
-        ldv<Real, V>(in + base0 + (int64_t)x * sx + (int64_t)r * sy, d[r]);
+        ldv<Real, V>(inw + ((int64_t)x * sx + (int64_t)r * sy) + lo_off, d[r]);
       } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) d[r][v] = Real(0);
@@ -160,9 +168,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
     for (int v = 0; v < V; ++v) b[v] = tp[v] = Real(0);
     e = Real(0);
     if (pl) {
-      if (hb_live) ldv<Real, V>(in + base0 + (int64_t)x * sx - sy, b);
-      if (ht_live) ldv<Real, V>(in + base0 + (int64_t)x * sx + (int64_t)R * sy, tp);
-      if (eload) e = in[ebase + (int64_t)x * sx];
+      const Real* pl0 = inw + (int64_t)x * sx;
+      if (hb_live) ldv<Real, V>(pl0 - sy + lo_off, b);
+      if (ht_live) ldv<Real, V>(pl0 + (int64_t)R * sy + lo_off, tp);
+      if (eload) e = pl0[eoff];
     }
   };
 
@@ -273,7 +282,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
                 m[s] = fmax(m[s], zst[v] ? d : 0.0);
                 nan_seen |= zst[v] && nv[v] != nv[v];
               }
-              Real* dst = out + base0 + (int64_t)p * sx + (int64_t)r * sy;
+              Real* dst = outw + ((int64_t)p * sx + (int64_t)r * sy) + lo_off;
               if (allst) {
                 stv<Real, V>(dst, nv);
               } else {
@@ -356,6 +365,19 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.xq = (int)(nblocks / 8);
   g.xr = (int)(nblocks % 8);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tbr: residual slots " << p.slot << "+" << K);
+  // Variants whose registers spill are slow and, with the ring fully unrolled,
+  // have been miscompiled on ROCm 7.2 (tr4:1:4:1:16:0:4 produced wrong row-0
+  // values); refuse them unless explicitly allowed.
+  static const int spill = [] {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q>)) == hipSuccess
+               ? (int)a.localSizeBytes
+               : 0;
+  }();
+  static const bool allow = std::getenv("HEAT3D_ALLOW_SPILL") && std::getenv("HEAT3D_ALLOW_SPILL")[0] == '1';
+  HEAT3D_CHECK(spill == 0 || allow, "tbr variant " << ks.str() << " spills " << spill
+                                                   << " B of registers per lane; pick a smaller tile / ring "
+                                                      "(HEAT3D_ALLOW_SPILL=1 overrides)");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
   hipLaunchKernelGGL((stencil_tbr<Real, V, R, WY, K, Q>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
@@ -378,6 +400,7 @@ static void dispatch_tbr(const StencilParams& p, const KernelSpec& k, hipStream_
 #define H3D_TBR_Q(VV, RR, YY, KK) H3D_TBR(VV, RR, YY, KK, 3) H3D_TBR(VV, RR, YY, KK, 4)
   H3D_TBR_Q(1, 4, 16, 2) H3D_TBR_Q(1, 4, 16, 3) H3D_TBR_Q(1, 4, 16, 4)
   H3D_TBR_Q(1, 4, 8, 3) H3D_TBR_Q(1, 4, 8, 4) H3D_TBR_Q(1, 6, 8, 3) H3D_TBR_Q(1, 3, 16, 3)
+  H3D_TBR_Q(1, 3, 16, 4) H3D_TBR_Q(1, 2, 16, 3) H3D_TBR_Q(1, 3, 16, 2)
   H3D_TBR_Q(1, 2, 16, 2) H3D_TBR_Q(2, 2, 8, 2) H3D_TBR_Q(2, 2, 16, 2)
   if constexpr (sizeof(Real) == 4) {
     H3D_TBR_Q(2, 4, 8, 3) H3D_TBR_Q(2, 4, 8, 4) H3D_TBR_Q(2, 4, 16, 3) H3D_TBR_Q(2, 4, 8, 2)

@@ -66,7 +66,9 @@ class Backend {
                           StreamId s) = 0;
   virtual void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
                         const Layout& Ld, const Box& bd, StreamId s) = 0;
-  virtual void check_convergence(DeviceState* st, int slot, StreamId s) = 0;
+  // convergence checks of `count` consecutive iterations, residual slots
+  // slot .. slot + count - 1, in order (one launch on the GPU)
+  virtual void check_convergence(DeviceState* st, int slot, StreamId s, int count = 1) = 0;
   virtual void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
                                 const int64_t gstart[3], double hy, DeviceState* st,
                                 StreamId s) = 0;

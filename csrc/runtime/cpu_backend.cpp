@@ -80,8 +80,8 @@ class CpuBackend final : public Backend {
                 const Layout& Ld, const Box& bd, StreamId) override {
     cpu::copy_box(t, src, Ls, bs, dst, Ld, bd);
   }
-  void check_convergence(DeviceState* st, int slot, StreamId) override {
-    cpu::check_convergence(st, slot);
+  void check_convergence(DeviceState* st, int slot, StreamId, int count) override {
+    for (int i = 0; i < count; ++i) cpu::check_convergence(st, slot + i);
   }
   void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
                         const int64_t gstart[3], double hy, DeviceState* st, StreamId) override {

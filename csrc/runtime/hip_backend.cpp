@@ -171,8 +171,8 @@ class HipBackend final : public Backend {
                 const Layout& Ld, const Box& bd, StreamId s) override {
     hip::copy_box(t, src, Ls, bs, dst, Ld, bd, streams_[s]);
   }
-  void check_convergence(DeviceState* st, int slot, StreamId s) override {
-    hip::check_convergence(st, slot, streams_[s]);
+  void check_convergence(DeviceState* st, int slot, StreamId s, int count) override {
+    hip::check_convergence(st, slot, streams_[s], count);
   }
   void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
                         const int64_t gstart[3], double hy, DeviceState* st, StreamId s) override {

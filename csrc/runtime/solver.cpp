@@ -89,12 +89,14 @@ KernelSpec KernelSpec::resolved(DType t) const {
       def(r.WY, f64 ? 16 : 8);
       def(r.NT, 1);  // prefetch depth
       break;
-    case TBR:  // same tiles as TBK; 7th field = T^n ring size (4: full-step prefetch)
-      def(r.V, f64 ? 1 : 2);
-      def(r.R, 4);
+    case TBR:  // 7th field = T^n ring size.  fp64: K = 2 32 x 128 tiles, K = 3
+               // 48 x 64, K >= 4 32 x 64 (8 waves); fp32: 32 x 128.  All
+               // without register spills (launch_tbr refuses spilling variants).
+      def(r.V, f64 ? (K == 2 ? 2 : 1) : 2);
+      def(r.R, f64 ? (K == 2 ? 2 : K == 3 ? 3 : 4) : 4);
       def(r.WZ, 1);
-      def(r.WY, f64 ? 16 : 8);
-      def(r.NT, 4);
+      def(r.WY, f64 ? (K <= 3 ? 16 : 8) : 8);
+      def(r.NT, 3);
       break;
     default:
       break;
@@ -150,13 +152,11 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
           : kspec2_.multi_step() ? kspec2_.K
           : dims[0] > 1 ? 2
                         : kDefaultTemporal;
-  if (kspec2_.kind == KernelSpec::TBR) {
-    // explicitly requested register-ring kernel: any depth
-  } else if (K == 2 && kspec2_.kind != KernelSpec::TBK) {
-    kspec2_.kind = KernelSpec::TB2;
-  } else {
-    kspec2_.kind = KernelSpec::TBK;
-  }
+  // default: the register-ring kernel (stencil_tbr.hip; MI355X 1024^3: fp64
+  // +5% at K = 3, +3% at K = 2; fp32 +18% / +15% over the queue kernels,
+  // profiles/kernel_sweep.md); tb2 / tbK select the queue kernels
+  if (!kspec2_.multi_step()) kspec2_.kind = KernelSpec::TBR;
+  if (kspec2_.kind == KernelSpec::TB2 && K != 2) kspec2_.kind = KernelSpec::TBK;
   kspec2_.K = K;
   int64_t min_n0 = INT64_MAX;
   for (const auto& sd : dec_.subs) min_n0 = std::min(min_n0, sd.n[0]);
@@ -499,7 +499,7 @@ void Solver::enqueue_multi(int bi) {
   auto reduce_and_check = [&](StreamId s) {
     if (!comm_->all_local() && comm_->size() > 1)
       comm_->allreduce(&dstate_->residual[0], K_, RedType::U64, RedOp::Max, *be_, s);
-    for (int i = 0; i < K_; ++i) be_->check_convergence(dstate_, i, s);
+    be_->check_convergence(dstate_, 0, s, K_);
   };
   if (!tb_overlap_) {
     ev_wait(kCompute, EV_CHK + 0);

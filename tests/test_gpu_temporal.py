@@ -104,10 +104,10 @@ def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
 
 
 VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb3:1:4:1:16", "tb3:1:6:1:8", "tb3:1:4:2:8", "tb3:1:4:1:8:3",
-                  "tr3", "tr3:1:4:1:16:0:3", "tr3:1:3:1:16:0:3", "tr3:1:4:1:8:0:4", "tr3:1:6:1:8:0:3", "tr3:1:4:1:8:5:3"],
-              4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1", "tr4", "tr4:1:4:1:8:0:3"],
+                  "tr3", "tr3:1:3:1:16:0:3", "tr3:1:4:1:8:0:4", "tr3:1:6:1:8:0:3", "tr3:1:4:1:8:5:3", "tr3:1:2:1:16:0:3"],
+              4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1", "tr4", "tr4:1:4:1:8:0:3", "tr4:1:4:1:8:0:4"],
               2: ["tbk2", "tbk2:2:2:1:8", "tr2", "tr2:2:2:1:8:0:3", "tr2:1:4:1:16:0:3", "tr2:2:2:1:16"]}
-VARIANTS_K_F32 = {3: ["tr3:2:4:1:8:0:3", "tr3:2:4:1:8:0:4", "tr3:2:4:1:16:0:4"], 4: ["tr4:2:4:1:8:0:4"],
+VARIANTS_K_F32 = {3: ["tr3:2:4:1:8:0:3", "tr3:2:4:1:8:0:4", "tr3:2:4:1:16:0:3"], 4: ["tr4:2:4:1:8:0:4"],
                   2: ["tr2:2:4:1:8:0:3", "tr2:2:4:1:8:0:4"]}
 
 
@@ -167,7 +167,7 @@ def _deep_random(ops, n, gx, dtype, seed):
 
 
 @pytest.mark.parametrize("kernel", ["tb2", "tbk2", "tb3", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb4", "tb4:1:6:1:8",
-                                    "tr2", "tr3", "tr3:1:4:1:16:0:3", "tr4", "tr2:2:2:1:8:0:3"])
+                                    "tr2", "tr3", "tr3:1:3:1:16:0:3", "tr4", "tr2:2:2:1:8:0:3"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (5, (0, 5), "lo"), (9, (0, 9), "hi"),
                                             (12, (4, 8), "both"), (12, (0, 4), "both"), (12, (8, 12), "both"),
@@ -219,7 +219,7 @@ def test_temporal_mixed_steps_gpu(h3d, gpu, K, vr):
     assert np.array_equal(a.gather(), b.gather())
 
 
-@pytest.mark.parametrize("kernel2", ["tr3", "tr3:1:4:1:16:0:3", "tr2", "tr4"])
+@pytest.mark.parametrize("kernel2", ["tr3", "tr3:1:4:1:8:0:3", "tr2", "tr4"])
 @pytest.mark.parametrize("vr", [1, 3])
 def test_ring_kernel_solver_gpu(h3d, gpu, kernel2, vr):
     """Register-ring sweeps (stencil_tbr.hip) in the solver, single domain and
