@@ -65,6 +65,27 @@ __device__ __forceinline__ float dpp_shl1(float old, float v) {
                                       0x130, 0xf, 0xf, false);
   return __builtin_bit_cast(float, r);
 }
+// Same shifts with the vacated lane (0 resp. 63) zero-filled (bound_ctrl):
+// no "old" operand, so no register copy in front of the DPP move.  For
+// neighbours whose edge lane is invalid anyway.
+__device__ __forceinline__ double dpp_shr1z(double v) {
+  long long vv = __builtin_bit_cast(long long, v);
+  int lo = __builtin_amdgcn_mov_dpp((int)vv, 0x138, 0xf, 0xf, true);
+  int hi = __builtin_amdgcn_mov_dpp((int)(vv >> 32), 0x138, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_shl1z(double v) {
+  long long vv = __builtin_bit_cast(long long, v);
+  int lo = __builtin_amdgcn_mov_dpp((int)vv, 0x130, 0xf, 0xf, true);
+  int hi = __builtin_amdgcn_mov_dpp((int)(vv >> 32), 0x130, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ float dpp_shr1z(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float dpp_shl1z(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
+}
 __device__ __forceinline__ double readlane(double v, int lane) {
   long long b = __builtin_bit_cast(long long, v);
   int lo = __builtin_amdgcn_readlane((int)b, lane);

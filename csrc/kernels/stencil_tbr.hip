@@ -121,30 +121,44 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   const int xe = min(xa + g.seg, g.bhi[0]);
   const int64_t sx = g.sx, sy = g.sy;
 
-  // per-lane column masks: in the box, stored, valid for the residual of stage s
+  // per-lane column masks: in the box, stored.  The residual's column
+  // validity (stage s: columns [s, TZ - s) of the tile) is applied once, to
+  // per-column accumulators at the end (kColAcc), instead of per point — except
+  // for V > 1 in 16-wave groups, where K x V accumulators overflow the
+  // 128-VGPR budget: those keep per-point masks.
+  constexpr bool kColAcc = V == 1 || WY * 64 <= 512;
+  constexpr int VA = kColAcc ? V : 1;  // residual accumulators per stage
   bool zin[V], zst[V];
   bool allst = true;
-  bool lres[K][V];  // stage s's residual counts this column
+  bool lres[kColAcc ? 1 : K][V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     const int kk = k + v, cp = lane * V + v;
     zin[v] = kk >= g.blo[2] && kk < g.bhi[2];
     zst[v] = zin[v] && cp >= g.zring && cp < TZ - g.zring;
     allst &= zst[v];
+    if constexpr (!kColAcc)
 #pragma unroll
-    for (int s = 0; s < K; ++s) lres[s][v] = zin[v] && cp >= s && cp < TZ - s;
+      for (int s = 0; s < K; ++s) lres[s][v] = zin[v] && cp >= s && cp < TZ - s;
   }
-  // uniform element offset of (plane 0, row yb, column tkb); lanes add lane * V
   const int64_t wbase = g.origin + (int64_t)yb * sy + tkb;
   const Real* __restrict__ inw = in + wbase;
   Real* __restrict__ outw = out + wbase;
   const int lo_off = lane * V;
+  // Loads are unconditional, with rows clamped to the ghosted layout [-1, yhi]
+  // and planes to [xlo_live, xhi_live]: a clamped value is a real (finite)
+  // field value standing in for a point outside the layout, and such points
+  // only ever feed copies outside the update box, never a stored value or a
+  // residual (no zero-fill moves, no per-row branches in the step).
+  // (32-bit: |row offset| <= (R + 1) * sy < 2^31, checked in launch_tbr)
+  auto crow = [&](int row) { return (min(max(row, -1), yhi) - yb) * (int)sy; };
+  int roff[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) roff[r] = crow(yb + r);
+  const int roff_lo = crow(yb - 1), roff_hi = crow(yb + R);
   const int er = lane & 31;
-  const bool eload = er < rlive && yb + er >= -1;
-  const int eoff = er * (int)sy + (lane < 32 ? -1 : TZ);  // halo column of row er
+  const int eoff = (min(max(yb + er, -1), yhi) - yb) * (int)sy + (lane < 32 ? -1 : TZ);  // halo column of row er
   const bool has_lo = wave > 0, has_hi = wave + 1 < WY;
-  const bool hb_live = !has_lo && yb - 1 >= -1 && rlive > 0;
-  const bool ht_live = !has_hi && yb + R <= yhi && rlive == R;
 
   // rings: T^n plane p and its y/z halo live in slot (p - x0 + 1) mod Q;
   // F_{s+1} produced at step x lives in f[s][(x - x0) mod 3]
@@ -152,27 +166,13 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   Real hb[Q][V], ht[Q][V], ed[Q];
   Real f[K - 1][QS][R][V];
 
-  auto plane_live = [&](int x) { return x >= g.xlo_live && x <= g.xhi_live; };
   auto load_plane = [&](int x, Real (&d)[R][V], Real (&b)[V], Real (&tp)[V], Real& e) {
-    const bool pl = plane_live(x);
+    const Real* pl0 = inw + (int64_t)min(max(x, g.xlo_live), g.xhi_live) * sx;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (pl && r < rlive && yb + r >= -1) {
-        ldv<Real, V>(inw + ((int64_t)x * sx + (int64_t)r * sy) + lo_off, d[r]);
-      } else {
-#pragma unroll
-        for (int v = 0; v < V; ++v) d[r][v] = Real(0);
-      }
-    }
-#pragma unroll
-    for (int v = 0; v < V; ++v) b[v] = tp[v] = Real(0);
-    e = Real(0);
-    if (pl) {
-      const Real* pl0 = inw + (int64_t)x * sx;
-      if (hb_live) ldv<Real, V>(pl0 - sy + lo_off, b);
-      if (ht_live) ldv<Real, V>(pl0 + (int64_t)R * sy + lo_off, tp);
-      if (eload) e = pl0[eoff];
-    }
+    for (int r = 0; r < R; ++r) ldv<Real, V>(pl0 + roff[r] + lo_off, d[r]);
+    if (!has_lo) ldv<Real, V>(pl0 + roff_lo + lo_off, b);
+    if (!has_hi) ldv<Real, V>(pl0 + roff_hi + lo_off, tp);
+    e = pl0[eoff];
   };
 
   const int x0 = xa - (K - 1);
@@ -188,10 +188,14 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
 #pragma unroll
         for (int v = 0; v < V; ++v) f[s][i][r][v] = Real(0);
 
-  double m[K];
+  double m[K][VA];
+  bool nan_seen[VA];
 #pragma unroll
-  for (int s = 0; s < K; ++s) m[s] = 0.0;
-  bool nan_seen = false;
+  for (int v = 0; v < VA; ++v) {
+    nan_seen[v] = false;
+#pragma unroll
+    for (int s = 0; s < K; ++s) m[s][v] = 0.0;
+  }
   int par = 0;
 
   // whole chunks of U steps (no early exit: the unrolled body needs a constant
@@ -249,17 +253,25 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
             // widened by K-1-s (possibly from halo planes still being
             // exchanged): never counted
             const bool rres = yin && xval && x <= xlast && rp >= s && rp < TYB - s;
-            const Real left = s == 0 ? readlane(ed[sC], r) : C[r][0];
-            const Real right = s == 0 ? readlane(ed[sC], 32 + r) : C[r][V - 1];
+            const Real left = s == 0 ? readlane(ed[sC], r) : Real(0);
+            const Real right = s == 0 ? readlane(ed[sC], 32 + r) : Real(0);
             const Real* ym = r == 0 ? lo : C[r > 0 ? r - 1 : 0];
             const Real* yp = r == R - 1 ? hi : C[r + 1 < R ? r + 1 : 0];
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-              const Real zm = v == 0 ? dpp_shr1(left, C[r][V - 1]) : C[r][v > 0 ? v - 1 : 0];
-              const Real zp = v == V - 1 ? dpp_shl1(right, C[r][0]) : C[r][v + 1 < V ? v + 1 : 0];
+              // stage 0: the tile's halo columns enter lanes 0 / 63; later
+              // stages: those lanes are outside the valid region anyway
+              const Real zm = v > 0 ? C[r][v > 0 ? v - 1 : 0]
+                              : s == 0 ? dpp_shr1(left, C[r][V - 1]) : dpp_shr1z(C[r][V - 1]);
+              const Real zp = v < V - 1 ? C[r][v + 1 < V ? v + 1 : 0]
+                              : s == 0 ? dpp_shl1(right, C[r][0]) : dpp_shl1z(C[r][0]);
               const Real nv = ftcs<Real>(C[r][v], M[r][v], P[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
               N[r][v] = (yin && zin[v]) ? nv : C[r][v];
-              if (rres) m[s] = fmax(m[s], lres[s][v] ? fabs((double)nv - (double)C[r][v]) : 0.0);
+              if (rres) {
+                const double d = fabs((double)nv - (double)C[r][v]);
+                if constexpr (kColAcc) m[s][v < VA ? v : 0] = fmax(m[s][v < VA ? v : 0], d);
+                else m[s][0] = fmax(m[s][0], lres[kColAcc ? 0 : s][v] ? d : 0.0);
+              }
             }
           }
         } else {
@@ -275,12 +287,17 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
               Real nv[V];
 #pragma unroll
               for (int v = 0; v < V; ++v) {
-                const Real zm = v == 0 ? dpp_shr1(C[r][0], C[r][V - 1]) : C[r][v > 0 ? v - 1 : 0];
-                const Real zp = v == V - 1 ? dpp_shl1(C[r][V - 1], C[r][0]) : C[r][v + 1 < V ? v + 1 : 0];
+                const Real zm = v > 0 ? C[r][v > 0 ? v - 1 : 0] : dpp_shr1z(C[r][V - 1]);
+                const Real zp = v < V - 1 ? C[r][v + 1 < V ? v + 1 : 0] : dpp_shl1z(C[r][0]);
                 nv[v] = ftcs<Real>(C[r][v], M[r][v], P[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
                 const double d = fabs((double)nv[v] - (double)C[r][v]);
-                m[s] = fmax(m[s], zst[v] ? d : 0.0);
-                nan_seen |= zst[v] && nv[v] != nv[v];
+                if constexpr (kColAcc) {
+                  m[s][v < VA ? v : 0] = fmax(m[s][v < VA ? v : 0], d);
+                  nan_seen[v < VA ? v : 0] |= nv[v] != nv[v];
+                } else {
+                  m[s][0] = fmax(m[s][0], zst[v] ? d : 0.0);
+                  nan_seen[0] |= zst[v] && nv[v] != nv[v];
+                }
               }
               Real* dst = outw + ((int64_t)p * sx + (int64_t)r * sy) + lo_off;
               if (allst) {
@@ -302,13 +319,27 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
     }
   }
   if (res) {
-    if (__any(nan_seen)) {
+    bool nan_any = false;
+    double mm[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) mm[s] = 0.0;
+#pragma unroll
+    for (int v = 0; v < VA; ++v) {
+      const int cp = lane * V + v;
+      nan_any |= (!kColAcc || zst[v]) && nan_seen[v];
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const bool ok = !kColAcc || (s == K - 1 ? zst[v] : (zin[v] && cp >= s && cp < TZ - s));
+        mm[s] = fmax(mm[s], ok ? m[s][v] : 0.0);
+      }
+    }
+    if (__any(nan_any)) {
       if (lane == 0)
 #pragma unroll
         for (int s = 0; s < K; ++s) atomicMax(res + s, 0x7ff8000000000000ULL);
     }
 #pragma unroll
-    for (int s = 0; s < K; ++s) residual_commit(res + s, m[s]);
+    for (int s = 0; s < K; ++s) residual_commit(res + s, mm[s]);
   }
 }
 
@@ -319,7 +350,7 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   constexpr int TYB = WY * R;
   const Layout& L = p.L;
   HEAT3D_CHECK(L.gx >= 1 && L.n[0] + 2 * L.gx < (1LL << 30) && L.n[1] + 2 < (1LL << 30) &&
-                   L.sy < (1LL << 30),
+                   L.sy * (TYB + 2) < (1LL << 31),
                "tbr: extents exceed 32-bit tile coordinates");
   TBRArgs g;
   g.sx = L.sx;
