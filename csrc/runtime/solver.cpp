@@ -146,16 +146,14 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   // else kDefaultTemporal.  Halos may only cross x faces (slabs, or one
   // subdomain) and travel K planes deep, so every subdomain needs >= K owned
   // planes.  Decided from the global decomposition so that every rank agrees.
-  // Auto depth: 3 for one subdomain; 2 for x slabs, whose K-plane boundary
-  // slabs cost more than the saved traffic at K = 3 (profiles/kernel_sweep.md)
-  int K = cfg_.temporal >= 2 ? cfg_.temporal
-          : kspec2_.multi_step() ? kspec2_.K
-          : dims[0] > 1 ? 2
-                        : kDefaultTemporal;
-  // default: the register-ring kernel (stencil_tbr.hip; MI355X 1024^3: fp64
-  // +5% at K = 3, +3% at K = 2; fp32 +18% / +15% over the queue kernels,
-  // profiles/kernel_sweep.md); tb2 / tbK select the queue kernels
-  if (!kspec2_.multi_step()) kspec2_.kind = KernelSpec::TBR;
+  // Auto depth: 3, for one subdomain and for x slabs alike (MI355X, 1024^3
+  // fp64 as 8 virtual x slabs on one GPU: K = 3 341 GLUPS vs K = 2 301 with the
+  // ring kernel; profiles/kernel_sweep.md)
+  int K = cfg_.temporal >= 2 ? cfg_.temporal : kspec2_.multi_step() ? kspec2_.K : kDefaultTemporal;
+  // default kernel: the register-ring kernel (stencil_tbr.hip; 1024^3 fp64
+  // tr3 621-640 vs tb3 551 GLUPS, fp32 1090 vs 884), except at K = 2 where the
+  // tuned queue kernel tb2 is faster (508 vs 490); tb2 / tbK / trK force one
+  if (!kspec2_.multi_step()) kspec2_.kind = K == 2 ? KernelSpec::TB2 : KernelSpec::TBR;
   if (kspec2_.kind == KernelSpec::TB2 && K != 2) kspec2_.kind = KernelSpec::TBK;
   kspec2_.K = K;
   int64_t min_n0 = INT64_MAX;
