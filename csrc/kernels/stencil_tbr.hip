@@ -157,6 +157,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   for (int r = 0; r < R; ++r) roff[r] = crow(yb + r);
   const int roff_lo = crow(yb - 1), roff_hi = crow(yb + R);
   const int er = lane & 31;
+  const bool eload = er < R;
   const int eoff = (min(max(yb + er, -1), yhi) - yb) * (int)sy + (lane < 32 ? -1 : TZ);  // halo column of row er
   const bool has_lo = wave > 0, has_hi = wave + 1 < WY;
 
@@ -172,7 +173,9 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
     for (int r = 0; r < R; ++r) ldv<Real, V>(pl0 + roff[r] + lo_off, d[r]);
     if (!has_lo) ldv<Real, V>(pl0 + roff_lo + lo_off, b);
     if (!has_hi) ldv<Real, V>(pl0 + roff_hi + lo_off, tp);
-    e = pl0[eoff];
+    // halo columns: lanes r and 32 + r (r < R) only — all 64 lanes would touch
+    // 64 different rows' cache lines per plane
+    if (eload) e = pl0[eoff];
   };
 
   const int x0 = xa - (K - 1);
