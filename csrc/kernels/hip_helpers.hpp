@@ -101,14 +101,51 @@ __device__ __forceinline__ float readlane(float v, int lane) {
 // blown-up field reaches the convergence check as a fault.
 __device__ __forceinline__ double res_max(double m, double d) { return (d != d || d > m) ? d : m; }
 
-__device__ __forceinline__ void residual_commit(unsigned long long* slot, double m) {
+__device__ __forceinline__ unsigned long long wave_max_bits(double m) {
   unsigned long long b = (unsigned long long)__builtin_bit_cast(long long, m);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long q = __shfl_xor(b, o, 64);
     b = q > b ? q : b;
   }
-  if ((threadIdx.x & 63) == 0) atomicMax(slot, b);
+  return b;
+}
+
+// Device-scope max into a residual slot.  The slot only grows during a
+// sweep, so a (possibly stale, hence never larger) relaxed read that is
+// already >= b makes the atomic redundant: most workgroups skip it.  All
+// workgroups of a grid finish at nearly the same time and agent-scope atomics
+// on one address serialise at the memory side, so unfiltered per-wave
+// atomics (1728 workgroups x 16 waves x K slots) cost ~0.5 ms per sweep.
+__device__ __forceinline__ void slot_max(unsigned long long* slot, unsigned long long b) {
+  if (b > __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(slot, b);
+}
+
+__device__ __forceinline__ void residual_commit(unsigned long long* slot, double m) {
+  const unsigned long long b = wave_max_bits(m);
+  if ((threadIdx.x & 63) == 0) slot_max(slot, b);
+}
+
+// Workgroup-level commit of K residual slots: one wave max per slot into LDS,
+// then lanes s < K of wave 0 reduce over the NW waves and commit once.  Must
+// be reached by every thread of the workgroup (contains a barrier).
+template <int NW, int K>
+__device__ __forceinline__ void residual_commit_block(unsigned long long* slots, const double (&m)[K],
+                                                      bool nan_any, unsigned long long (&red)[NW][K]) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool nan_w = __any(nan_any);
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    const unsigned long long b = wave_max_bits(m[s]);
+    if (lane == 0) red[wave][s] = nan_w ? 0x7ff8000000000000ULL : b;
+  }
+  __syncthreads();
+  if (wave == 0 && lane < K) {
+    unsigned long long b = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) b = red[w][lane] > b ? red[w][lane] : b;
+    slot_max(slots + lane, b);
+  }
 }
 
 __device__ __forceinline__ bool flag_set(const int* done) {

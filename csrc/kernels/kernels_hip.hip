@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 
 #include "hip_helpers.hpp"
 
@@ -384,12 +385,34 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tile(const Real* __restr
 }
 
 // Resident workgroups of `kernel` on the whole device (occupancy x CUs).
+// hipOccupancyMaxActiveBlocksPerMultiprocessor over-reports for kernels with
+// large static LDS (it returned 8 x 1024-thread groups per CU for the 98 KiB
+// tr3 kernel, which fits once in the 160 KiB of a CU), so the result is capped
+// by our own LDS / wave-slot / VGPR bound.  HEAT3D_TRACE=1 prints both.
 int device_slots(const void* kernel, int block) {
-  int dev = 0, cus = 256, per = 1;
-  if (hipGetDevice(&dev) == hipSuccess)
+  int dev = 0, cus = 256, per = 1, lds_cu = 160 * 1024;
+  if (hipGetDevice(&dev) == hipSuccess) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) == hipSuccess && v > 0)
+      lds_cu = v;
+  }
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess || per < 1) per = 1;
-  return std::max(1, cus * per);
+  int own = 64;
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, kernel) == hipSuccess) {
+    const int waves = (block + 63) / 64;
+    if (a.sharedSizeBytes > 0) own = std::min<int>(own, lds_cu / (int)a.sharedSizeBytes);
+    // 4 SIMDs x 512 VGPRs per lane (granule 8), at most 8 waves per SIMD
+    const int vg = std::max(8, (a.numRegs + 7) / 8 * 8);
+    const int per_simd = std::min(8, 512 / vg);
+    own = std::min(own, (4 * per_simd) / std::max(1, waves));
+  }
+  const int pick = std::max(1, std::min(per, own));
+  if (std::getenv("HEAT3D_TRACE"))
+    std::fprintf(stderr, "[heat3d trace] device_slots: cus=%d api=%d own=%d lds=%zu vgpr=%d -> %d/CU\n", cus, per,
+                 own, (size_t)a.sharedSizeBytes, a.numRegs, pick);
+  return std::max(1, cus * pick);
 }
 
 // x-segment length for an x-marching kernel.  Each segment re-reads two

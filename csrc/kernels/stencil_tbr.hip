@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "hip_helpers.hpp"
@@ -96,6 +97,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   static_assert(TYB > 2 * (K - 1) && R <= 32, "tile too small");
   // centre-plane bottom/top rows of every stage, double-buffered by step parity
   __shared__ __attribute__((aligned(16))) Real s_row[2][K][WY][2][TZ];
+  __shared__ unsigned long long s_red[WY][K];  // per-wave residual maxima
   if (flag_set(done)) return;
 
   const int blk = blockIdx.x;
@@ -336,13 +338,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
         mm[s] = fmax(mm[s], ok ? m[s][v] : 0.0);
       }
     }
-    if (__any(nan_any)) {
-      if (lane == 0)
-#pragma unroll
-        for (int s = 0; s < K; ++s) atomicMax(res + s, 0x7ff8000000000000ULL);
-    }
-#pragma unroll
-    for (int s = 0; s < K; ++s) residual_commit(res + s, mm[s]);
+    residual_commit_block<WY, K>(res, mm, nan_any, s_red);
   }
 }
 
@@ -398,6 +394,9 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(nblocks < (1LL << 31), "too many blocks");
   g.xq = (int)(nblocks / 8);
   g.xr = (int)(nblocks % 8);
+  if (std::getenv("HEAT3D_TRACE"))
+    std::fprintf(stderr, "[heat3d trace] tbr K=%d box x %lld: seg=%d tiles=%dx%d blocks=%lld\n", K,
+                 (long long)b.extent(0), g.seg, g.nzb, g.nyb, (long long)nblocks);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tbr: residual slots " << p.slot << "+" << K);
   // Variants whose registers spill are slow and, with the ring fully unrolled,
   // have been miscompiled on ROCm 7.2 (tr4:1:4:1:16:0:4 produced wrong row-0
