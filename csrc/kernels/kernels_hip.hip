@@ -681,6 +681,17 @@ void check_convergence(DeviceState* s, int slot, void* stream, int count) {
   HIPK_CHECK(hipGetLastError());
 }
 
+__global__ void delay_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void delay(double us, void* stream) {
+  if (us <= 0) return;
+  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, S(stream), (unsigned long long)(us * 100.0));
+  HIPK_CHECK(hipGetLastError());
+}
+
 // ---- error vs analytic steady state T = y -------------------------------------
 constexpr int kErrBlocks = 1024;
 int64_t error_scratch_elems() { return kErrBlocks; }

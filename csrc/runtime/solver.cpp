@@ -164,12 +164,20 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   halo_depth_ = tb_ && dims[0] > 1 ? K : 1;
   // overlapped sweeps need a non-empty interior between the boundary slabs
   tb_overlap_ = tb_ && dims[0] > 1 && overlap_ && min_n0 >= 2 * K + 1;
+  // lagged convergence check (third buffer, two residual-slot banks) keeps
+  // the all-reduce + check off the critical path of the overlapped sweeps
+  {
+    const char* e = std::getenv("HEAT3D_LAG");
+    lag_ = tb_overlap_ && 2 * K_ <= kResidualSlots && !(e && e[0] == '0');
+  }
+  nbuf_ = lag_ ? 3 : 2;
+  if (const char* e = std::getenv("HEAT3D_FAKE_ALLREDUCE_US")) fake_allreduce_us_ = std::atof(e);
 
   for (int r : comm_->local_ranks()) {
     Local l;
     l.sd = dec_.subs[r];
     l.L = Layout::make(l.sd.n, (int64_t)esize_, halo_depth_);
-    for (int b = 0; b < 2; ++b) l.field[b] = be_->alloc(l.L.bytes());
+    for (int b = 0; b < nbuf_; ++b) l.field[b] = be_->alloc(l.L.bytes());
     for (int a = 0; a < 3; ++a) {
       l.owned.lo[a] = 0;
       l.owned.hi[a] = l.sd.n[a];
@@ -211,7 +219,8 @@ Solver::~Solver() {
   for (auto& e : tev_)
     if (e) be_->event_destroy(e);
   for (auto& l : local_) {
-    for (auto* f : l.field) be_->release(f);
+    for (auto* f : l.field)
+      if (f) be_->release(f);
     for (auto& io : l.faces) {
       be_->release(io.sendbuf);
       be_->release(io.recvbuf);
@@ -308,7 +317,7 @@ void Solver::initialize() {
   }
   for (auto& l : local_) {
     InitParams p = init_params(l);
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < nbuf_; ++b) {
       p.field = l.field[b];
       be_->init_field(dt_, p, kCompute);
     }
@@ -325,7 +334,8 @@ void Solver::initialize() {
   be_->copy(dstate_, hstate_, sizeof(DeviceState), CopyKind::H2D, kCompute);
   be_->sync(kCompute);
   issued_ = 0;
-  phase_ = 0;
+  cur_ = 0;
+  nsweep_ = 0;
   last_kind_ = 0;
   segs_.clear();
   seg_head_ = 0;
@@ -405,7 +415,7 @@ void Solver::enqueue_iteration(int p, int bi) {
   auto params = [&](Local& l, const Box& b) {
     StencilParams sp;
     sp.in = l.field[bi];
-    sp.out = l.field[bi ^ 1];
+    sp.out = l.field[nxt(bi)];
     sp.L = l.L;
     sp.box = b;
     for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
@@ -470,34 +480,43 @@ void Solver::enqueue_iteration(int p, int bi) {
 // the rollback in finalize_converged().
 //
 // Single subdomain: everything on the compute stream (graph-capturable).
-// x slabs (sweeps alternate buffers, so pipeline events are indexed by bi):
-//   compute: wait check+boundary(prev sweep) - interior planes [K, n0-K) - INT
-//   comm   : K-plane halo of T^t - wait interior+check(prev) - boundary slabs - BND
+// x slabs (pipeline events indexed by sweep parity q):
+//   compute: wait check(q-L) + boundary(q-1) - interior planes [K, n0-K) - INT
+//   comm   : K-plane halo of T^t - wait interior(q-1) + check(q-L) - boundary slabs - BND
 //   reduce : wait INT, BND - allreduce(max) of the K residual slots - K checks - CHK
 // The halo of sweep k+1 only depends on sweep k's boundary slabs, so it
-// overlaps sweep k's interior tail and its all-reduce.
+// overlaps sweep k's interior tail and its all-reduce.  L = 1 with two
+// buffers; with three (lag_) L = 2: the all-reduce and check of sweep q run
+// under sweep q+1, whose residuals go to the other slot bank; if sweep q
+// converged, q+1 was speculative (its output buffer is not q's input) and
+// q+2 onwards are no-ops.  Exchanged values stay bitwise identical.
 void Solver::enqueue_multi(int bi) {
   H3D_TRACE("sweep" << K_ << " issued=" << issued_ << " buf=" << bi << (capturing_ ? " (capturing)" : ""));
   HEAT3D_CHECK(tb_, "temporal blocking not enabled for this decomposition");
   if (last_kind_ != 2) join_pipeline();
   last_kind_ = 2;
+  // lagged schedule: events and residual slots alternate by sweep parity
+  const int q = lag_ ? (int)(nsweep_ & 1) : bi;
+  const int slot0 = lag_ ? q * K_ : 0;
   auto params = [&](Local& l, const Box& b) {
     StencilParams sp;
     sp.in = l.field[bi];
-    sp.out = l.field[bi ^ 1];
+    sp.out = l.field[nxt(bi)];
     sp.L = l.L;
     sp.box = b;
     for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
     sp.state = dstate_;
-    sp.slot = 0;
+    sp.slot = slot0;
     sp.ux[0] = l.ux[0];
     sp.ux[1] = l.ux[1];
     return sp;
   };
   auto reduce_and_check = [&](StreamId s) {
     if (!comm_->all_local() && comm_->size() > 1)
-      comm_->allreduce(&dstate_->residual[0], K_, RedType::U64, RedOp::Max, *be_, s);
-    be_->check_convergence(dstate_, 0, s, K_);
+      comm_->allreduce(&dstate_->residual[slot0], K_, RedType::U64, RedOp::Max, *be_, s);
+    else if (fake_allreduce_us_ > 0)
+      be_->delay(fake_allreduce_us_, s);  // single-GPU stand-in for the RCCL latency
+    be_->check_convergence(dstate_, slot0, s, K_);
   };
   if (!tb_overlap_) {
     ev_wait(kCompute, EV_CHK + 0);
@@ -517,10 +536,16 @@ void Solver::enqueue_multi(int bi) {
     ev_record(EV_CHK + 1, kCompute);
     return;
   }
-  const int q = bi;
+  // Which check must precede this sweep's writes: it overwrites buffer
+  // nxt(bi), the input of sweep q-1 (2 buffers) or q-2 (3 buffers), which a
+  // convergence inside that sweep needs for the rollback; the same check
+  // resets the residual slots this sweep writes.  EV_CHK + (q ^ 1) is sweep
+  // q-1's check in both schedules' indexing; with the lag, EV_CHK + q still
+  // stands for sweep q-2's (q's is recorded below).
+  const int chk_prev = lag_ ? q : (q ^ 1);
   // [A] interior planes
-  ev_wait(kCompute, EV_CHK + (q ^ 1));  // previous sweep's checks: done flag, slots reset
-  ev_wait(kCompute, EV_BND + (q ^ 1));  // its boundary slabs are part of our input
+  ev_wait(kCompute, EV_CHK + chk_prev);
+  ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of our input
   be_->range_push("interior");
   for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), kspec2_, kCompute);
   be_->range_pop();
@@ -528,7 +553,7 @@ void Solver::enqueue_multi(int bi) {
   // [B] deep halo, then the boundary slabs
   enqueue_halo(bi, kComm);
   ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
-  ev_wait(kComm, EV_CHK + (q ^ 1));
+  ev_wait(kComm, EV_CHK + chk_prev);
   be_->range_push("boundary");
   for (auto& l : local_)
     for (const Box& b : l.tb_boundary) be_->stencil2(dt_, params(l, b), kspec2_, kComm);
@@ -539,6 +564,7 @@ void Solver::enqueue_multi(int bi) {
   ev_wait(kReduce, EV_BND + q);
   reduce_and_check(kReduce);
   ev_record(EV_CHK + q, kReduce);
+  ++nsweep_;
 }
 
 void Solver::join_pipeline() {
@@ -565,18 +591,19 @@ void Solver::finalize_converged(int64_t c) {
   HEAT3D_CHECK(hit, "segment of converged iteration " << c << " not recorded");
   const Segment s = *hit;
   const int m = (int)(c - s.start + 1);  // steps of the segment that are wanted
-  int final_buf = s.inbuf ^ 1;
+  int final_buf = nxt(s.inbuf);
   if (m < s.len) {
     // The sweep's input buffer still holds T^start with its K-deep halo (the
     // later, no-op sweeps only re-exchanged unchanged faces into it).  Redo
     // m forced single steps; step j also updates m-j halo planes on faces
     // with a neighbour, so no exchange is needed in between.
     for (int j = 1; j <= m; ++j) {
-      const int src = (j & 1) ? s.inbuf : s.inbuf ^ 1;
+      const int src = (j & 1) ? s.inbuf : nxt(s.inbuf);
+      const int dst = (j & 1) ? nxt(s.inbuf) : s.inbuf;
       for (auto& l : local_) {
         StencilParams sp;
         sp.in = l.field[src];
-        sp.out = l.field[src ^ 1];
+        sp.out = l.field[dst];
         sp.L = l.L;
         sp.box = l.owned;
         const int64_t w = m - j;
@@ -588,10 +615,10 @@ void Solver::finalize_converged(int64_t c) {
       }
     }
     be_->sync(kCompute);
-    final_buf = s.inbuf ^ (m & 1);
+    final_buf = (m & 1) ? nxt(s.inbuf) : s.inbuf;
   }
   issued_ = c + 1;
-  phase_ = (int)((final_buf - (c + 1)) & 1);
+  cur_ = final_buf;
 }
 
 void Solver::accumulate_phase_times() {
@@ -669,7 +696,7 @@ void Solver::run_chunk(int64_t n) {
     const char* e = std::getenv("HEAT3D_GRAPH_MULTISTREAM");
     return e && e[0] == '1';
   }();
-  const bool graphs = cfg_.use_graph && be_->supports_graphs() && comm_->capturable() &&
+  const bool graphs = cfg_.use_graph && be_->supports_graphs() && comm_->capturable() && nbuf_ == 2 &&
                       !graph_failed_ && !phase_timing_ && (!multi_stream() || ms_ok);
   const int want_kind = tb_ ? 2 : 1;
   while (n > 0) {
@@ -694,12 +721,13 @@ void Solver::run_chunk(int64_t n) {
           for (int i = 0; i < graph_iters_ / K_; ++i) {
             record_segment(issued_, K_, cur());
             issued_ += K_;
-            phase_ ^= (K_ + 1) & 1;  // a K-step sweep flips the buffer once
+            cur_ = nxt(cur_);
           }
         } else {
           for (int i = 0; i < graph_iters_; ++i) {
             record_segment(issued_, 1, cur());
             ++issued_;
+            cur_ = nxt(cur_);
           }
         }
         n -= graph_iters_;
@@ -715,7 +743,7 @@ void Solver::run_chunk(int64_t n) {
       record_segment(issued_, K_, cur());
       enqueue_multi(cur());
       issued_ += K_;
-      phase_ ^= (K_ + 1) & 1;  // a K-step sweep flips the buffer once
+      cur_ = nxt(cur_);
       n -= K_;
       continue;
     }
@@ -725,6 +753,7 @@ void Solver::run_chunk(int64_t n) {
     enqueue_iteration((int)(issued_ & 1), cur());
     if (phase_timing_) accumulate_phase_times();
     ++issued_;
+    cur_ = nxt(cur_);
     --n;
   }
 }
@@ -1067,7 +1096,7 @@ void Solver::load_checkpoint(const std::string& dir) {
       }
     void* stage = be_->alloc(host.size());
     be_->copy(stage, host.data(), host.size(), CopyKind::H2D, kCompute);
-    for (int b = 0; b < 2; ++b) be_->unpack_box(dt_, l.field[b], l.L, lb, stage, kCompute);
+    for (int b = 0; b < nbuf_; ++b) be_->unpack_box(dt_, l.field[b], l.L, lb, stage, kCompute);
     be_->sync(kCompute);
     be_->release(stage);
   }
@@ -1082,7 +1111,7 @@ void Solver::load_checkpoint(const std::string& dir) {
   be_->copy(dstate_, hstate_, sizeof(DeviceState), CopyKind::H2D, kCompute);
   be_->sync(kCompute);
   issued_ = it;
-  phase_ = 0;
+  cur_ = 0;
 }
 
 int Solver::verify_halos() {
@@ -1090,7 +1119,7 @@ int Solver::verify_halos() {
   if (issued_ == 0 || !has_halo_) return 0;
   // input buffer of the last iteration (or pair): its ghosts were filled by
   // that exchange from the neighbours' (unchanged) faces
-  const int p = cur() ^ 1;
+  const int p = prv(cur());
   int nf = 0;
   for (auto& l : local_) nf += (int)l.faces.size();
   auto* dsum = static_cast<unsigned long long*>(be_->alloc(sizeof(unsigned long long) * 3 * nf));
@@ -1168,7 +1197,7 @@ void Solver::inject(int idx, int64_t i, int64_t j, int64_t k, double value, bool
   auto& l = local_.at(idx);
   HEAT3D_CHECK(i >= -1 && i <= l.sd.n[0] && j >= -1 && j <= l.sd.n[1] && k >= -1 && k <= l.sd.n[2],
                "inject index outside the ghosted block");
-  be_->poke(dt_, l.field[cur() ^ (previous ? 1 : 0)], l.L, i, j, k, value, kCompute);
+  be_->poke(dt_, l.field[previous ? prv(cur()) : cur()], l.L, i, j, k, value, kCompute);
   be_->sync(kCompute);
 }
 

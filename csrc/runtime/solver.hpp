@@ -107,6 +107,8 @@ class Solver {
   // subdomain, or x slabs with K-plane halos); K = temporal_steps().
   bool temporal_blocking() const { return tb_; }
   int temporal_steps() const { return K_; }
+  // field buffers per subdomain (3 = lagged convergence check of overlapped sweeps)
+  int field_buffers() const { return nbuf_; }
 
   // Output / checkpoint.
   void write_tecplot(const std::string& path, const std::string& layout);
@@ -145,7 +147,7 @@ class Solver {
   struct Local {
     Subdomain sd;
     Layout L;
-    void* field[2] = {nullptr, nullptr};
+    void* field[3] = {nullptr, nullptr, nullptr};  // nbuf_ of them in use
     Box owned, interior;
     std::vector<Box> shell;
     std::vector<FaceIO> faces;
@@ -164,8 +166,11 @@ class Solver {
   void enqueue_halo(int bi, StreamId s);
   void join_pipeline();      // every stream waits for every pipeline event
   bool multi_stream() const { return tb_ ? tb_overlap_ : overlap_; }
-  // buffer holding T^{issued_}
-  int cur() const { return (int)((issued_ + phase_) & 1); }
+  // buffer holding T^{issued_}; a step or a K-step sweep reads cur() and
+  // writes nxt(cur())
+  int cur() const { return cur_; }
+  int nxt(int b) const { return b + 1 == nbuf_ ? 0 : b + 1; }
+  int prv(int b) const { return b == 0 ? nbuf_ - 1 : b - 1; }
   void record_segment(int64_t start, int len, int inbuf);
   void finalize_converged(int64_t conv_iter);
   void poll_enqueue(StreamId s);
@@ -193,8 +198,15 @@ class Solver {
   DeviceState* dstate_ = nullptr;   // device
   DeviceState* hstate_ = nullptr;   // pinned host mirror
   int64_t issued_ = 0;              // iterations enqueued so far (absolute index)
-  // T^t lives in field[(t + phase_) & 1]; a 2-step sweep flips phase_
-  int phase_ = 0;
+  int cur_ = 0;               // buffer holding T^{issued_}
+  // Field buffers: 2 (ping-pong), or 3 for overlapped x-slab sweeps, where the
+  // convergence check of sweep q (all-reduce + check kernel) is lagged: sweep
+  // q+1 runs speculatively into the third buffer and only sweep q+2, which
+  // overwrites sweep q's input (needed for a rollback), waits for it.
+  int nbuf_ = 2;
+  bool lag_ = false;
+  int64_t nsweep_ = 0;
+  double fake_allreduce_us_ = 0;  // diagnostic: emulated all-reduce latency (virtual ranks)        // overlapped sweeps issued (event / residual-slot parity)
   bool tb_ = false;           // K-step temporal blocking active
   int K_ = 1;                 // iterations per sweep
   KernelSpec kspec2_;

@@ -128,3 +128,23 @@ def test_cpu_sweep_definition(h3d, K, box_x, ux):
         T = T.clone()
         T[lo + K: hi + K, 1:-1, 1:-1] = new
     assert torch.equal(out.owned()[box_x[0]:box_x[1]], T[box_x[0] + K: box_x[1] + K, 1:-1, 1:-1])
+
+
+@pytest.mark.parametrize("K", [2, 3, 4])
+def test_lagged_check_uses_three_buffers(h3d, K, monkeypatch):
+    """Overlapped x-slab sweeps lag the convergence check by one sweep (third
+    field buffer, two residual-slot banks); HEAT3D_LAG=0 restores the
+    ping-pong schedule.  Both converge at the same iteration to the same field,
+    with the converged iteration landing at every offset inside a sweep."""
+    for eps in (1e-3, 9e-4, 8e-4, 7e-4):
+        a, b = _pair(h3d, (37, 21, 19), 10 ** 6, eps, 3, K=K, extra=["--check-every", "5"])
+        assert a.native.field_buffers == 3
+        monkeypatch.setenv("HEAT3D_LAG", "0")
+        c = h3d.HeatSolver((37, 21, 19), 10 ** 6, eps, backend="cpu", virtual_ranks=3, decomp=(3, 1, 1),
+                           extra_args=["--temporal", str(K), "--check-every", "5"])
+        monkeypatch.delenv("HEAT3D_LAG")
+        assert c.native.field_buffers == 2 and b.native.field_buffers == 2
+        ra, rb, rc = a.run(), b.run(), c.run()
+        assert ra["conv_iter"] == rb["conv_iter"] == rc["conv_iter"] and ra["converged"]
+        ref = b.gather()
+        assert np.array_equal(a.gather(), ref) and np.array_equal(c.gather(), ref), (K, eps)
