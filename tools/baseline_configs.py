@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--timeout", type=int, default=900)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--md-out", default="", help="also write the markdown table (profiles/baseline_configs.md)")
     a = ap.parse_args()
     rows = []
     real = a.gpus >= 8
@@ -105,6 +106,27 @@ def main():
     if a.json_out:
         with open(a.json_out, "w") as f:
             json.dump(rows, f, indent=1)
+    if a.md_out:
+        with open(a.md_out, "w") as f:
+            f.write(markdown(rows))
+
+
+def markdown(rows):
+    out = ["| # | config | mode | dtype | grid | parallelism | kernel | GLUPS | ms/step | time-to-converge |",
+           "|---|---|---|---|---|---|---|---|---|---|"]
+    for r in rows:
+        if r["config"] == 1:
+            out.append(f"| 1 | {r['name']} | {r['mode']} | fp64 | 64^3 | 1 rank, OpenMP | cpu | {r['glups']} | — | "
+                       f"{r['iterations']} it (golden {r['golden_iterations']}) in {r['time_to_converge_s']} s at "
+                       f"eps {r['eps']:g}, error {r['error_percent']} % (golden {r['golden_error']}) |")
+            continue
+        for b in (r["bench"] if isinstance(r["bench"], list) else [r["bench"]]):
+            c = b["config"]
+            t = b.get("time_to_converge")
+            ttc = (f"{t['iterations']} it in {t['seconds']:.3f} s at eps {t['eps']:g}" if t else "—")
+            out.append(f"| {r['config']} | {r['name']} | {r['mode']} | {b['dtype']} | {'x'.join(map(str, c['grid']))} | "
+                       f"{c['parallelism']} | `{c['kernel']}` | {b['value']} | {b['ms_per_step']} | {ttc} |")
+    return "\n".join(out) + "\n"
 
 
 if __name__ == "__main__":
