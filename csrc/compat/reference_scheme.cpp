@@ -63,7 +63,7 @@ void ReferenceScheme::step(int64_t) {
   const int64_t cx = c_[0], cy = c_[1], cz = c_[2];
   const int64_t sx = cy * cz, sy = cz;
   auto upd = [&](double c, double xm, double xp, double ym, double yp, double zm, double zp) {
-    return ((c + Dx * ((xp - 2.0 * c) + xm)) + Dy * ((yp - 2.0 * c) + ym)) + Dz * ((zp - 2.0 * c) + zm);
+    return ftcs_update<double>(c, xm, xp, ym, yp, zm, zp, Dx, Dy, Dz);
   };
   for (auto& rk : ranks_) rk.T0 = rk.T;  // heat3D.cu:543-548
   const int P = (int)ranks_.size();

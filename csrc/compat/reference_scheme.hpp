@@ -21,7 +21,7 @@
 //     (heat3D.cu:1093-1106).
 //
 // ReferenceScheme runs all ranks of that scheme in one process (host, OpenMP),
-// with the reference's per-cell expression order and contraction disabled,
+// with the reference's per-cell expression (kernels.hpp ftcs_update),
 // so its iteration counts can be checked against SURVEY.md App. B.3b
 // (27^3, eps 1e-5: 2513 / 2511 / 2543 / 2615 iterations for 1x1x1 / 2x1x1 /
 // 2x2x1 / 2x2x2).  It is the `--scheme reference` mode of the CLI; it exists

@@ -27,17 +27,13 @@ template <> struct VecOf<float, 1> { typedef float type; };
 template <> struct VecOf<float, 2> { typedef float type __attribute__((ext_vector_type(2))); };
 template <> struct VecOf<float, 4> { typedef float type __attribute__((ext_vector_type(4))); };
 
-// FTCS 7-point update in the reference's expression order (heat3D.cu:128-131),
-// contraction off: bitwise identical to the CPU backend.
+// FTCS 7-point update (heat3D.cu:128-131) with the reference GPU kernel's
+// FMA contraction; the single definition lives in kernels.hpp (ftcs_update)
+// and is shared with the CPU backend, so fields stay bitwise identical.
 template <typename Real>
 __device__ __forceinline__ Real ftcs(Real c, Real xm, Real xp, Real ym, Real yp, Real zm, Real zp,
                                      Real Dx, Real Dy, Real Dz) {
-#pragma clang fp contract(off)
-  const Real c2 = Real(2) * c;
-  const Real ax = (xp - c2) + xm;
-  const Real ay = (yp - c2) + ym;
-  const Real az = (zp - c2) + zm;
-  return ((c + Dx * ax) + Dy * ay) + Dz * az;
+  return ftcs_update<Real>(c, xm, xp, ym, yp, zm, zp, Dx, Dy, Dz);
 }
 
 // ---- cross-lane helpers ----------------------------------------------------

@@ -2,9 +2,10 @@
 //   heat3d::hip::*  hand-written gfx950 kernels (kernels_hip.hip)
 //   heat3d::cpu::*  OpenMP host kernels used by the CPU backend / oracle (kernels_cpu.cpp)
 //
-// Both evaluate the FTCS update with the reference's per-cell expression order
-// (heat3D.cu:128-131) and with floating-point contraction
-// disabled, so the GPU and CPU backends agree bit for bit.
+// Both evaluate the FTCS update through ftcs_update() below: the reference's
+// per-cell expression (heat3D.cu:128-131) with the fused
+// multiply-adds nvcc puts into the reference's GPU kernel, explicit, and no
+// other contraction, so the GPU and CPU backends agree bit for bit.
 #pragma once
 
 #include <cstdint>
@@ -129,6 +130,25 @@ unsigned long long box_bitsum(DType t, const void* f, const Layout& L, const Box
 // Shared scalar logic of the convergence check (heat3D.cu:1026-1073 with the
 // survey's fixes: global norm, global max residual).  Used verbatim by the
 // CPU backend and mirrored by the single-thread HIP kernel.
+// FTCS 7-point update of heat3D.cu:128-131,
+//   T + Dx*(T[i+1] - 2T + T[i-1]) + Dy*(...) + Dz*(...),
+// evaluated the way nvcc compiles it for the reference's GPU kernel (default
+// -fmad=true): left to right, every "acc + D*a" contracted to one fused
+// multiply-add, and "T[i+1] - 2T" to fma(-2, T, T[i+1]) (2T is exact, so that
+// one is the same value either way).  Written with explicit fused operations
+// so that the CPU backend (libm fma, correctly rounded) and every gfx950
+// kernel (v_fma_f64 / v_fma_f32) produce bitwise identical fields.
+H3D_HD inline double h3d_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+H3D_HD inline float h3d_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+template <typename Real>
+H3D_HD inline Real ftcs_update(Real c, Real xm, Real xp, Real ym, Real yp, Real zm, Real zp, Real Dx,
+                               Real Dy, Real Dz) {
+  const Real ax = h3d_fma(Real(-2), c, xp) + xm;
+  const Real ay = h3d_fma(Real(-2), c, yp) + ym;
+  const Real az = h3d_fma(Real(-2), c, zp) + zm;
+  return h3d_fma(Dz, az, h3d_fma(Dy, ay, h3d_fma(Dx, ax, c)));
+}
+
 H3D_HD inline void check_convergence_scalar(DeviceState* s, double r) {
   const int64_t t = s->iter;
   if (s->hist_cap > 0) s->hist[t % s->hist_cap] = r;

@@ -3,12 +3,14 @@
 // This is the "64^3 fp64 CPU Jacobi reference" of BASELINE.json config 1 and
 // the bitwise oracle for the gfx950 kernels.  Unlike the reference CPU twin
 // (heat3D.cpp:606-612, whose interior update block is empty — SURVEY A9) it
-// updates every owned point.  Compile with -ffp-contract=off.
+// updates every owned point.  Compile with -ffp-contract=off (the update's
+// fused multiply-adds are explicit, kernels.hpp ftcs_update).
 #include <omp.h>
 
 #include <cmath>
 #include <cstring>
 
+#include "cpu_rows.hpp"
 #include "kernels.hpp"
 
 namespace heat3d {
@@ -60,24 +62,17 @@ static void stencil_t(const StencilParams& p) {
   // max |dT| reduced on the IEEE bit patterns of the non-negative doubles so
   // that a NaN (bits above +Inf) propagates to the convergence check
   unsigned long long resbits = 0;
+  const auto rowfn = [] {
+    if constexpr (sizeof(Real) == 8) return cpu_row_kernels().f64;
+    else return cpu_row_kernels().f32;
+  }();
+  const int64_t nk = b.extent(2);
 #pragma omp parallel for collapse(2) schedule(static) reduction(max : resbits)
   for (int64_t i = b.lo[0]; i < b.hi[0]; ++i)
     for (int64_t j = b.lo[1]; j < b.hi[1]; ++j) {
-      const int64_t base = L.index(i, j, 0);
-      double lres = 0.0;
-      for (int64_t k = b.lo[2]; k < b.hi[2]; ++k) {
-        const int64_t c = base + k;
-        const Real T = in[c];
-        const Real T2 = Real(2) * T;
-        // heat3D.cu:128-131 expression order
-        const Real ax = (in[c + sx] - T2) + in[c - sx];
-        const Real ay = (in[c + sy] - T2) + in[c - sy];
-        const Real az = (in[c + 1] - T2) + in[c - 1];
-        const Real nv = ((T + Dx * ax) + Dy * ay) + Dz * az;
-        out[c] = nv;
-        const double d = std::fabs(static_cast<double>(nv) - static_cast<double>(T));
-        lres = (d != d || d > lres) ? d : lres;
-      }
+      const int64_t c = L.index(i, j, b.lo[2]);
+      // heat3D.cu:128-131 with nvcc's FMA contraction (kernels.hpp ftcs_update)
+      const double lres = nk > 0 ? rowfn(in + c, out + c, nk, sx, sy, Dx, Dy, Dz) : 0.0;
       unsigned long long bits;
       std::memcpy(&bits, &lres, sizeof(bits));
       resbits = bits > resbits ? bits : resbits;

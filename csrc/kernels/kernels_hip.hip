@@ -22,8 +22,9 @@
 //     one 64-bit atomic max per wave;
 //   * a device flag set by the convergence check turns the kernel into a
 //     no-op, so over-issued / graph-replayed iterations are harmless.
-// Floating-point contraction is disabled so results are bitwise identical to
-// the CPU backend (kernels_cpu.cpp) and independent of the decomposition.
+// Implicit contraction is disabled and the update's FMAs are explicit
+// (ftcs_update), so results are bitwise identical to the CPU backend
+// (kernels_cpu.cpp) and independent of the decomposition.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

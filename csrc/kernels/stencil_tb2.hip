@@ -5,7 +5,7 @@
 // intermediate u = T^{n+1} of its tile in registers (a second x-queue next to
 // the T^n queue) and writes only T^{n+2}, i.e. 8 B read + 8 B written per point
 // per TWO iterations.  Every point still goes through the reference update
-// twice, in the same expression order and without contraction, so T^{n+2}
+// twice, with the same arithmetic (kernels.hpp ftcs_update), so T^{n+2}
 // and both residuals are bitwise identical to two single-step sweeps
 // (tests/test_gpu_kernels.py).
 //

@@ -8,7 +8,7 @@
 // are produced and only F_K is written.  Per point and per K iterations the
 // kernel reads T^n once and writes T^{n+K} once: 16 B / K per iteration in
 // fp64 instead of 16 B.  Every F_s value goes through the reference update
-// (heat3D.cu:128-131) in the same expression order with contraction off, so
+// (heat3D.cu:128-131) with the same arithmetic (kernels.hpp ftcs_update), so
 // T^{n+K} and all K residuals are bitwise identical to K single steps.
 //
 // Tiles overlap: F_1 is valid on the whole (WY*R rows) x (WZ*64*V columns)

@@ -3,7 +3,7 @@
 // Same algorithm and bitwise results as stencil_tbk.hip (one HBM sweep turns
 // T^n into T^{n+K}; stage s turns F_s = T^{n+s} into F_{s+1}, lagging stage
 // s-1 by one plane; every point goes through the reference update,
-// heat3D.cu:128-131, in the same expression order with contraction off), but
+// heat3D.cu:128-131, with the same arithmetic (kernels.hpp ftcs_update)), but
 // restructured after the rocprofv3 counters of stencil_tbk on MI355X
 // (profiles/pmc_tbk.md, profiles/kernel_sweep.md): there, 28% of the wave cycles issued, 45%
 // waited, and of the VALU stream ~10% were plain register moves rotating
@@ -67,22 +67,24 @@ __device__ __forceinline__ void ldv(const Real* p, Real (&d)[V]) {
   }
 }
 
-template <typename Real, int V>
+template <typename Real, int V, bool NTS = false>
 __device__ __forceinline__ void stv(Real* p, const Real (&s)[V]) {
   if constexpr (V == 1) {
-    *p = s[0];
+    if constexpr (NTS) __builtin_nontemporal_store(s[0], p);
+    else *p = s[0];
   } else {
     typedef typename VecOf<Real, V>::type Vec;
     Vec t;
 #pragma unroll
     for (int v = 0; v < V; ++v) t[v] = s[v];
-    *reinterpret_cast<Vec*>(p) = t;
+    if constexpr (NTS) __builtin_nontemporal_store(t, reinterpret_cast<Vec*>(p));
+    else *reinterpret_cast<Vec*>(p) = t;
   }
 }
 
 }  // namespace
 
-template <typename Real, int V, int R, int WY, int K, int Q>
+template <typename Real, int V, int R, int WY, int K, int Q, bool NTS>
 __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ in,
                                                        Real* __restrict__ out, TBRArgs g,
                                                        Real Dx, Real Dy, Real Dz,
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
               }
               Real* dst = outw + ((int64_t)p * sx + (int64_t)r * sy) + lo_off;
               if (allst) {
-                stv<Real, V>(dst, nv);
+                stv<Real, V, NTS>(dst, nv);
               } else {
 #pragma unroll
                 for (int v = 0; v < V; ++v)
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   }
 }
 
-template <typename Real, int V, int R, int WY, int K, int Q>
+template <typename Real, int V, int R, int WY, int K, int Q, bool NTS>
 static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   const Box& b = p.box;
   constexpr int TZ = 64 * V;
@@ -381,7 +383,7 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   if (seg <= 0) {
     static int slots = 0;
     if (!slots)
-      slots = device_slots(reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q>), 64 * WY);
+      slots = device_slots(reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q, NTS>), 64 * WY);
     seg = choose_segment(b.extent(0), (int64_t)g.nzb * g.nyb, slots, 2 * K);
     // a segment runs seg + 2(K-1) steps in chunks of U = lcm(Q, 3)
     constexpr int U = Q == 3 ? 3 : 12;
@@ -403,7 +405,7 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   // values); refuse them unless explicitly allowed.
   static const int spill = [] {
     hipFuncAttributes a{};
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q>)) == hipSuccess
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q, NTS>)) == hipSuccess
                ? (int)a.localSizeBytes
                : 0;
   }();
@@ -413,7 +415,7 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
                                                       "(HEAT3D_ALLOW_SPILL=1 overrides)");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
-  hipLaunchKernelGGL((stencil_tbr<Real, V, R, WY, K, Q>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+  hipLaunchKernelGGL((stencil_tbr<Real, V, R, WY, K, Q, NTS>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
                      static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0],
                      (Real)p.D[1], (Real)p.D[2], r, done);
   HIPK_CHECK(hipGetLastError());
@@ -424,21 +426,33 @@ static void dispatch_tbr(const StencilParams& p, const KernelSpec& k, hipStream_
   const int K = k.K;
   const KernelSpec r = k.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
   const int V = r.V, R = r.R, WY = r.WY, Q = r.NT;
+  const bool nts = r.O == 1;  // 8th spec field: 1 = non-temporal T^{n+K} stores
   HEAT3D_CHECK(r.WZ == 1, "tbr kernels span the tile's z extent with one wave (WZ = 1)");
-#define H3D_TBR(VV, RR, YY, KK, QQ)                            \
-  if (V == VV && R == RR && WY == YY && K == KK && Q == QQ) {  \
-    launch_tbr<Real, VV, RR, YY, KK, QQ>(p, k, s);             \
-    return;                                                    \
+#define H3D_TBR(VV, RR, YY, KK, QQ)                                 \
+  if (V == VV && R == RR && WY == YY && K == KK && Q == QQ && !nts) { \
+    launch_tbr<Real, VV, RR, YY, KK, QQ, false>(p, k, s);             \
+    return;                                                         \
+  }
+  // variants also built with non-temporal output stores
+#define H3D_TBRN(VV, RR, YY, KK, QQ)                                \
+  H3D_TBR(VV, RR, YY, KK, QQ)                                       \
+  if (V == VV && R == RR && WY == YY && K == KK && Q == QQ && nts) {  \
+    launch_tbr<Real, VV, RR, YY, KK, QQ, true>(p, k, s);              \
+    return;                                                         \
   }
 #define H3D_TBR_Q(VV, RR, YY, KK) H3D_TBR(VV, RR, YY, KK, 3) H3D_TBR(VV, RR, YY, KK, 4)
+  H3D_TBRN(1, 3, 16, 3, 3) H3D_TBRN(1, 6, 8, 3, 3) H3D_TBRN(2, 2, 16, 2, 3)
   H3D_TBR_Q(1, 4, 16, 2) H3D_TBR_Q(1, 4, 16, 3) H3D_TBR_Q(1, 4, 16, 4)
-  H3D_TBR_Q(1, 4, 8, 3) H3D_TBR_Q(1, 4, 8, 4) H3D_TBR_Q(1, 6, 8, 3) H3D_TBR_Q(1, 3, 16, 3)
-  H3D_TBR_Q(1, 3, 16, 4) H3D_TBR_Q(1, 2, 16, 3) H3D_TBR_Q(1, 3, 16, 2)
-  H3D_TBR_Q(1, 2, 16, 2) H3D_TBR_Q(2, 2, 8, 2) H3D_TBR_Q(2, 2, 16, 2)
+  H3D_TBR_Q(1, 4, 8, 3) H3D_TBR_Q(1, 4, 8, 4) H3D_TBR(1, 6, 8, 4, 3) H3D_TBR(1, 3, 16, 4, 3)
+  H3D_TBR(1, 3, 16, 3, 4) H3D_TBR_Q(1, 2, 16, 3) H3D_TBR_Q(1, 3, 16, 2)
+  H3D_TBR_Q(1, 2, 16, 2) H3D_TBR_Q(2, 2, 8, 2) H3D_TBR(2, 2, 16, 2, 4)
+  H3D_TBR(1, 2, 16, 4, 3) H3D_TBR(2, 2, 8, 3, 3) H3D_TBR(1, 5, 8, 3, 3)
   if constexpr (sizeof(Real) == 4) {
-    H3D_TBR_Q(2, 4, 8, 3) H3D_TBR_Q(2, 4, 8, 4) H3D_TBR_Q(2, 4, 16, 3) H3D_TBR_Q(2, 4, 8, 2)
+    H3D_TBRN(2, 4, 8, 3, 3) H3D_TBRN(1, 4, 8, 4, 3) H3D_TBR(2, 4, 8, 3, 4)
+    H3D_TBR_Q(2, 4, 8, 4) H3D_TBR_Q(2, 4, 16, 3) H3D_TBR_Q(2, 4, 8, 2)
   }
 #undef H3D_TBR_Q
+#undef H3D_TBRN
 #undef H3D_TBR
   HEAT3D_THROW("unsupported tbr kernel variant V=" << V << " R=" << R << " WY=" << WY << " K=" << K
                                                    << " Q=" << Q);

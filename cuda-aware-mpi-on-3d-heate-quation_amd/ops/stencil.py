@@ -5,8 +5,8 @@ block + one-cell ghost shell, z fastest, rows padded so the first owned z
 point is 128-byte aligned) is allocated as a flat torch tensor; ``PaddedField``
 exposes strided views of it.  ``ftcs_step`` launches the hand-written gfx950
 kernel on torch's current HIP stream (or the OpenMP kernel for CPU tensors);
-``ftcs_reference`` is the plain-PyTorch oracle with the reference's
-expression order (heat3D.cu:128-131).
+``ftcs_reference`` is the plain-PyTorch oracle of the same arithmetic
+(heat3D.cu:128-131 with nvcc's FMA contraction, emulated exactly).
 """
 from __future__ import annotations
 
@@ -160,13 +160,15 @@ def unpack_box(f: PaddedField, box: Sequence[int], buf: torch.Tensor) -> None:
 
 
 def ftcs_reference(T: torch.Tensor, D: Sequence[float]) -> Tuple[torch.Tensor, float]:
-    """Plain-PyTorch FTCS on a ghosted block; returns (new interior, max |dT|)."""
+    """Plain-PyTorch FTCS on a ghosted block; returns (new interior, max |dT|).
+
+    Same arithmetic as the native backends (exactly rounded FMAs emulated with
+    error-free transformations, utils/fma.py), so results compare bitwise."""
+    from ..utils.fma import ftcs_update
+
     c = T[1:-1, 1:-1, 1:-1]
-    c2 = 2.0 * c
-    ax = (T[2:, 1:-1, 1:-1] - c2) + T[:-2, 1:-1, 1:-1]
-    ay = (T[1:-1, 2:, 1:-1] - c2) + T[1:-1, :-2, 1:-1]
-    az = (T[1:-1, 1:-1, 2:] - c2) + T[1:-1, 1:-1, :-2]
-    new = ((c + D[0] * ax) + D[1] * ay) + D[2] * az
+    new = ftcs_update(c, T[:-2, 1:-1, 1:-1], T[2:, 1:-1, 1:-1], T[1:-1, :-2, 1:-1], T[1:-1, 2:, 1:-1],
+                      T[1:-1, 1:-1, :-2], T[1:-1, 1:-1, 2:], D)
     res = (new.double() - c.double()).abs().max().item() if new.numel() else 0.0
     return new, res
 

@@ -5,9 +5,10 @@ tensor ops and torch.distributed point-to-point halos, independent of the
 native code: same decomposition rule (interior points split evenly, one-cell
 ghost shells), same per-point expression order (heat3D.cu:128-131), same
 convergence logic (norm = iteration-0 global residual, stop when
-global max residual / norm < eps).  Torch evaluates each elementwise op with
-one rounding and no FMA contraction, so on CPU the field is bitwise identical
-to the native backends.  Works with gloo (CPU) and nccl (GPU).
+global max residual / norm < eps).  The update's fused multiply-adds (nvcc's
+contraction of heat3D.cu:128-131, as in the native backends) are emulated
+exactly with error-free transformations (utils/fma.py), so on CPU the field
+is bitwise identical to the native backends.  Works with gloo (CPU) and nccl (GPU).
 """
 from __future__ import annotations
 
@@ -20,12 +21,11 @@ from .topology import decompose, dims_create
 
 def ftcs_update(T: torch.Tensor, D: Sequence[float]) -> torch.Tensor:
     """New values of the interior of a ghosted block ``T`` (shape n+2)."""
+    from ..utils.fma import ftcs_update as upd
+
     c = T[1:-1, 1:-1, 1:-1]
-    c2 = 2.0 * c
-    ax = (T[2:, 1:-1, 1:-1] - c2) + T[:-2, 1:-1, 1:-1]
-    ay = (T[1:-1, 2:, 1:-1] - c2) + T[1:-1, :-2, 1:-1]
-    az = (T[1:-1, 1:-1, 2:] - c2) + T[1:-1, 1:-1, :-2]
-    return ((c + D[0] * ax) + D[1] * ay) + D[2] * az
+    return upd(c, T[:-2, 1:-1, 1:-1], T[2:, 1:-1, 1:-1], T[1:-1, :-2, 1:-1], T[1:-1, 2:, 1:-1],
+               T[1:-1, 1:-1, :-2], T[1:-1, 1:-1, 2:], D)
 
 
 def boundary_grid(N: Sequence[int], dtype=torch.float64) -> torch.Tensor:

@@ -1,8 +1,9 @@
 """gfx950 kernel numerics vs a plain-PyTorch reference of the same op.
 
-Floating-point contraction is disabled in the kernels, so the HIP result must
-equal the torch CPU evaluation of the reference expression order
-(heat3D.cu:128-131) bit for bit, fp64 and fp32, for every kernel variant.
+The kernels evaluate heat3D.cu:128-131 with explicit fused multiply-adds in
+nvcc's contraction order (kernels.hpp ftcs_update) and no implicit
+contraction, so the HIP result must equal the torch CPU evaluation (exact FMA
+emulation, utils/fma.py) bit for bit, fp64 and fp32, for every kernel variant.
 """
 import pytest
 import torch
