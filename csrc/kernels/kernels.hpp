@@ -49,6 +49,8 @@ struct StencilParams {
   // neighbour halo); outside it they stay T^n (Dirichlet ghosts).
   // ux1 < ux0 means "the box's x range".
   int64_t ux[2] = {0, -1};
+  // same for y and z (block decompositions with deep y / z halos)
+  int64_t uy[2] = {0, -1}, uz[2] = {0, -1};
 };
 
 struct InitParams {

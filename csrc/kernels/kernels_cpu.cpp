@@ -27,11 +27,13 @@ static void init_t(const InitParams& p) {
   // every ghost plane (deep x halos included) gets its Dirichlet ghost rows
 #pragma omp parallel for collapse(2) schedule(static)
   for (int64_t i = -L.gx; i < L.n[0] + L.gx; ++i)
-    for (int64_t j = -1; j <= L.n[1]; ++j) {
+    for (int64_t j = -L.gy; j < L.n[1] + L.gy; ++j) {
       const int64_t gi = p.gstart[0] + i, gj = p.gstart[1] + j;
-      if (gi < 0 || gi >= p.N[0]) continue;
-      for (int64_t k = -1; k <= L.n[2]; ++k) {
+      // deep ghosts beyond the domain stay 0 (never read by an update)
+      if (gi < 0 || gi >= p.N[0] || gj < 0 || gj >= p.N[1]) continue;
+      for (int64_t k = -L.gz; k < L.n[2] + L.gz; ++k) {
         const int64_t gk = p.gstart[2] + k;
+        if (gk < 0 || gk >= p.N[2]) continue;
         const bool phys = gi == 0 || gi == p.N[0] - 1 || gj == 0 || gj == p.N[1] - 1 ||
                           gk == 0 || gk == p.N[2] - 1;
         f[L.index(i, j, k)] =
@@ -89,17 +91,20 @@ void stencil_multi(DType t, const StencilParams& p, int K, bool tb2_slots, void*
   void* scratch[2] = {scratch0, scratch1};
   std::memcpy(scratch[0], p.in, p.L.bytes());
   std::memcpy(scratch[1], p.in, p.L.bytes());
-  const bool wide = p.ux[1] >= p.ux[0];
+  const int64_t* u[3] = {p.ux, p.uy, p.uz};
   for (int s = 0; s < K; ++s) {
     StencilParams a = p;
     a.in = s == 0 ? p.in : scratch[(s - 1) & 1];
     a.out = s == K - 1 ? p.out : scratch[s & 1];
     a.slot = tb2_slots ? (s ? p.slot ^ 1 : p.slot) : p.slot + s;
-    if (wide) {
-      const int64_t w = K - 1 - s;
-      a.box.lo[0] = std::max(p.box.lo[0] - w, p.ux[0]);
-      a.box.hi[0] = std::min(p.box.hi[0] + w, p.ux[1]);
-    }
+    // stage s computes the box widened by K-1-s into the deep halos (the
+    // update range u of each axis), so that stage K-1 covers the box
+    for (int ax = 0; ax < 3; ++ax)
+      if (u[ax][1] >= u[ax][0]) {
+        const int64_t w = K - 1 - s;
+        a.box.lo[ax] = std::max(p.box.lo[ax] - w, u[ax][0]);
+        a.box.hi[ax] = std::min(p.box.hi[ax] + w, u[ax][1]);
+      }
     stencil(t, a);
   }
 }

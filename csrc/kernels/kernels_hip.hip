@@ -587,12 +587,13 @@ void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream)
 // ---- init ---------------------------------------------------------------------
 template <typename Real>
 __global__ __launch_bounds__(256) void init_kernel(Real* f, Layout L, InitParams p) {
-  const int64_t ez = L.n[2] + 2;
+  const int64_t ez = L.n[2] + 2 * L.gz;
   const int64_t kk = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (kk >= ez) return;
-  const int64_t k = kk - 1, j = (int64_t)blockIdx.y - 1, i = (int64_t)blockIdx.z - L.gx;
+  const int64_t k = kk - L.gz, j = (int64_t)blockIdx.y - L.gy, i = (int64_t)blockIdx.z - L.gx;
   const int64_t gi = p.gstart[0] + i, gj = p.gstart[1] + j, gk = p.gstart[2] + k;
-  if (gi < 0 || gi >= p.N[0]) return;  // deep ghost plane beyond the domain
+  // deep ghosts beyond the domain stay 0 (never read by an update)
+  if (gi < 0 || gi >= p.N[0] || gj < 0 || gj >= p.N[1] || gk < 0 || gk >= p.N[2]) return;
   const bool phys = gi == 0 || gi == p.N[0] - 1 || gj == 0 || gj == p.N[1] - 1 || gk == 0 ||
                     gk == p.N[2] - 1;
   f[L.index(i, j, k)] = phys ? (Real)boundary_value(gi, gj, gk, p.N, p.h) : Real(0);
@@ -601,7 +602,7 @@ __global__ __launch_bounds__(256) void init_kernel(Real* f, Layout L, InitParams
 void init_field(DType t, const InitParams& p, void* stream) {
   HIPK_CHECK(hipMemsetAsync(p.field, 0, p.L.bytes(), S(stream)));
   // every ghost plane (deep x halos included) gets its Dirichlet ghost rows
-  dim3 grid((unsigned)((p.L.n[2] + 2 + 255) / 256), (unsigned)(p.L.n[1] + 2),
+  dim3 grid((unsigned)((p.L.n[2] + 2 * p.L.gz + 255) / 256), (unsigned)(p.L.n[1] + 2 * p.L.gy),
             (unsigned)(p.L.n[0] + 2 * p.L.gx));
   if (t == DType::F64)
     hipLaunchKernelGGL(init_kernel<double>, grid, dim3(256), 0, S(stream),

@@ -24,32 +24,36 @@ struct Layout {
   int64_t origin = 0;        // element index of owned (0,0,0)
   int64_t elems = 0;         // allocation length in elements (includes tail pad)
   int64_t esize = 8;
-  int64_t gx = 1;            // ghost planes on each x side (1 or 2)
+  int64_t gx = 1;            // ghost planes on each x side (K with deep halos)
+  int64_t gy = 1, gz = 1;    // ghost rows / columns on each y / z side
 
-  // i in [-gx, n0 + gx - 1], j, k in [-1, n] (ghost shell included)
+  // i in [-gx, n0 + gx - 1], j in [-gy, n1 + gy - 1], k in [-gz, n2 + gz - 1]
   H3D_HD inline int64_t index(int64_t i, int64_t j, int64_t k) const {
     return origin + i * sx + j * sy + k;
   }
   // Alignment in elements used for the row offset / pitch.
   static int64_t align_elems(int64_t esize) { return 128 / esize; }
-  static Layout make(const int64_t n[3], int64_t esize, int64_t gx = 1) {
+  static Layout make(const int64_t n[3], int64_t esize, int64_t gx = 1, int64_t gy = 1, int64_t gz = 1) {
     Layout L;
     L.gx = gx;
+    L.gy = gy;
+    L.gz = gz;
     for (int a = 0; a < 3; ++a) L.n[a] = n[a];
     L.esize = esize;
     const int64_t A = align_elems(esize);
     L.zoff = A;                                  // ghost k = -1 lives at A - 1
-    const int64_t need = A + n[2] + 1;           // through ghost k = nz
+    if (gz > A) L.zoff = (gz + A - 1) / A * A;   // deep z ghosts (never with K <= 6)
+    const int64_t need = L.zoff + n[2] + gz;     // through ghost k = nz + gz - 1
     L.sy = ((need + A - 1) / A) * A;
     // break power-of-two row pitches (HBM channel / cache-set aliasing)
     if ((L.sy & (L.sy - 1)) == 0) L.sy += A;
-    L.sx = (n[1] + 2) * L.sy;
-    L.origin = gx * L.sx + L.sy + L.zoff;
+    L.sx = (n[1] + 2 * gy) * L.sy;
+    L.origin = gx * L.sx + gy * L.sy + L.zoff;
     // tail pad: kernels may over-read up to one 256-wide z tile past a row end
     L.elems = (n[0] + 2 * gx) * L.sx + 2 * L.sy + 1024;
     return L;
   }
-  // element offset of the start of x plane i (its ghost row j = -1)
+  // element offset of the start of x plane i (its ghost row j = -gy)
   H3D_HD inline int64_t plane_offset(int64_t i) const { return (gx + i) * sx; }
   std::size_t bytes() const { return static_cast<std::size_t>(elems * esize); }
 };

@@ -43,7 +43,10 @@ struct TBRArgs {
   int64_t sx, sy, origin;  // plane / row strides, element index of owned (0,0,0)
   int blo[3], bhi[3];      // store box
   int ulo, uhi;            // x range where F_{s+1} = FTCS(F_s)
+  int uylo, uyhi;          // same in y (box range unless deep y halos)
+  int uzlo, uzhi;          // same in z
   int xlo_live, xhi_live;  // x planes present in memory
+  int ylo_live, yhi_live;  // y rows present in memory
   int kb0, yb0;            // first column / row of tile (0, 0)
   int zstep, zring;        // tile stride along z, stored column ring
   int nzb, nyb, seg;
@@ -119,8 +122,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   const int tyb = g.yb0 + ybk * (TYB - 2 * (K - 1));    // tile's first row
   const int k = tkb + lane * V;
   const int yb = tyb + wave * R;
-  const int ylo = g.blo[1], yhi = g.bhi[1];
-  const int rlive = max(0, min(R, yhi + 1 - yb));  // rows <= yhi are loaded
+  const int uylo = g.uylo, uyhi = g.uyhi;
   const int xa = g.blo[0] + xs * g.seg;
   const int xe = min(xa + g.seg, g.bhi[0]);
   const int64_t sx = g.sx, sy = g.sy;
@@ -132,14 +134,16 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   // 128-VGPR budget: those keep per-point masks.
   constexpr bool kColAcc = V == 1 || WY * 64 <= 512;
   constexpr int VA = kColAcc ? V : 1;  // residual accumulators per stage
+  // zin: column in the update range (the box, or wider into deep z halos);
+  // zst: column stored by this tile (in the box)
   bool zin[V], zst[V];
   bool allst = true;
   bool lres[kColAcc ? 1 : K][V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     const int kk = k + v, cp = lane * V + v;
-    zin[v] = kk >= g.blo[2] && kk < g.bhi[2];
-    zst[v] = zin[v] && cp >= g.zring && cp < TZ - g.zring;
+    zin[v] = kk >= g.uzlo && kk < g.uzhi;
+    zst[v] = kk >= g.blo[2] && kk < g.bhi[2] && cp >= g.zring && cp < TZ - g.zring;
     allst &= zst[v];
     if constexpr (!kColAcc)
 #pragma unroll
@@ -149,20 +153,20 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   const Real* __restrict__ inw = in + wbase;
   Real* __restrict__ outw = out + wbase;
   const int lo_off = lane * V;
-  // Loads are unconditional, with rows clamped to the ghosted layout [-1, yhi]
-  // and planes to [xlo_live, xhi_live]: a clamped value is a real (finite)
+  // Loads are unconditional, with rows clamped to the ghosted layout
+  // [ylo_live, yhi_live] and planes to [xlo_live, xhi_live]: a clamped value is a real (finite)
   // field value standing in for a point outside the layout, and such points
   // only ever feed copies outside the update box, never a stored value or a
   // residual (no zero-fill moves, no per-row branches in the step).
   // (32-bit: |row offset| <= (R + 1) * sy < 2^31, checked in launch_tbr)
-  auto crow = [&](int row) { return (min(max(row, -1), yhi) - yb) * (int)sy; };
+  auto crow = [&](int row) { return (min(max(row, g.ylo_live), g.yhi_live) - yb) * (int)sy; };
   int roff[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) roff[r] = crow(yb + r);
   const int roff_lo = crow(yb - 1), roff_hi = crow(yb + R);
   const int er = lane & 31;
   const bool eload = er < R;
-  const int eoff = (min(max(yb + er, -1), yhi) - yb) * (int)sy + (lane < 32 ? -1 : TZ);  // halo column of row er
+  const int eoff = (min(max(yb + er, g.ylo_live), g.yhi_live) - yb) * (int)sy + (lane < 32 ? -1 : TZ);  // halo column of row er
   const bool has_lo = wave > 0, has_hi = wave + 1 < WY;
 
   // rings: T^n plane p and its y/z halo live in slot (p - x0 + 1) mod Q;
@@ -255,7 +259,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             const int row = yb + r, rp = wave * R + r;
-            const bool yin = xin && row >= ylo && row < yhi;
+            const bool yin = xin && row >= uylo && row < uyhi;
             // padded steps past xlast compute planes beyond the sweep's box
             // widened by K-1-s (possibly from halo planes still being
             // exchanged): never counted
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               const int row = yb + r, rp = wave * R + r;
-              const bool rst = row >= ylo && row < yhi && rp >= K - 1 && rp < TYB - (K - 1);
+              const bool rst = row >= g.blo[1] && row < g.bhi[1] && rp >= K - 1 && rp < TYB - (K - 1);
               if (!rst) continue;
               const Real* ym = r == 0 ? lo : C[r > 0 ? r - 1 : 0];
               const Real* yp = r == R - 1 ? hi : C[r + 1 < R ? r + 1 : 0];
@@ -350,8 +354,8 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   constexpr int TZ = 64 * V;
   constexpr int TYB = WY * R;
   const Layout& L = p.L;
-  HEAT3D_CHECK(L.gx >= 1 && L.n[0] + 2 * L.gx < (1LL << 30) && L.n[1] + 2 < (1LL << 30) &&
-                   L.sy * (TYB + 2) < (1LL << 31),
+  HEAT3D_CHECK(L.gx >= 1 && L.n[0] + 2 * L.gx < (1LL << 30) && L.n[1] + 2 * L.gy < (1LL << 30) &&
+                   L.sy * (TYB + 2 * L.gy) < (1LL << 31),
                "tbr: extents exceed 32-bit tile coordinates");
   TBRArgs g;
   g.sx = L.sx;
@@ -365,6 +369,17 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.uhi = (int)(p.ux[1] >= p.ux[0] ? p.ux[1] : b.hi[0]);
   g.xlo_live = (int)-L.gx;
   g.xhi_live = (int)(L.n[0] + L.gx - 1);
+  g.ylo_live = (int)-L.gy;
+  g.yhi_live = (int)(L.n[1] + L.gy - 1);
+  const bool wy = p.uy[1] >= p.uy[0], wz = p.uz[1] >= p.uz[0];
+  g.uylo = (int)(wy ? p.uy[0] : b.lo[1]);
+  g.uyhi = (int)(wy ? p.uy[1] : b.hi[1]);
+  g.uzlo = (int)(wz ? p.uz[0] : b.lo[2]);
+  g.uzhi = (int)(wz ? p.uz[1] : b.hi[2]);
+  // stage 0 reads one row / column beyond the update range
+  HEAT3D_CHECK(g.uylo - 1 >= -L.gy && g.uyhi <= L.n[1] + L.gy && g.uylo <= b.lo[1] && g.uyhi >= b.hi[1] &&
+                   g.uzlo - 1 >= -L.gz && g.uzhi <= L.n[2] + L.gz && g.uzlo <= b.lo[2] && g.uzhi >= b.hi[2],
+               "tbr: y/z update range outside the ghosted layout");
   HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live && g.ulo <= b.lo[0] &&
                    g.uhi >= b.hi[0],
                "tbr: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");

@@ -145,9 +145,12 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
 
   // K-step temporal blocking: on by default on the GPU, opt-in on the CPU
   // backend (tests).  Depth K from --temporal K, else from --kernel2 tbK,
-  // else kDefaultTemporal.  Halos may only cross x faces (slabs, or one
-  // subdomain) and travel K planes deep, so every subdomain needs >= K owned
-  // planes.  Decided from the global decomposition so that every rank agrees.
+  // else kDefaultTemporal.  Halos travel K planes / rows / columns deep, so
+  // every subdomain needs >= K owned points along each split axis.  y / z
+  // splits (block decompositions) need the register-ring kernel (the only one
+  // with y / z update ranges) and an axis-ordered exchange that also fills
+  // the edge and corner ghosts a K-step update reads.  Decided from the
+  // global decomposition so that every rank agrees.
   // Auto depth: 3, for one subdomain and for x slabs alike (MI355X, 1024^3
   // fp64 as 8 virtual x slabs on one GPU: K = 3 341 GLUPS vs K = 2 301 with the
   // ring kernel; profiles/kernel_sweep.md)
@@ -158,14 +161,26 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   if (!kspec2_.multi_step()) kspec2_.kind = K == 2 ? KernelSpec::TB2 : KernelSpec::TBR;
   if (kspec2_.kind == KernelSpec::TB2 && K != 2) kspec2_.kind = KernelSpec::TBK;
   kspec2_.K = K;
-  int64_t min_n0 = INT64_MAX;
-  for (const auto& sd : dec_.subs) min_n0 = std::min(min_n0, sd.n[0]);
-  tb_ = kspec_.kind != KernelSpec::Naive && (cfg_.temporal >= 2 || (cfg_.temporal == 0 && be_->is_gpu())) &&
-        dims[1] == 1 && dims[2] == 1 && (dims[0] == 1 || min_n0 >= K);
+  int64_t min_n[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
+  for (const auto& sd : dec_.subs)
+    for (int a = 0; a < 3; ++a) min_n[a] = std::min(min_n[a], sd.n[a]);
+  const int64_t min_n0 = min_n[0];
+  const bool block = dims[1] > 1 || dims[2] > 1;
+  bool fits = true;
+  for (int a = 0; a < 3; ++a) fits &= dims[a] == 1 || min_n[a] >= K;
+  tb_ = kspec_.kind != KernelSpec::Naive && (cfg_.temporal >= 2 || (cfg_.temporal == 0 && be_->is_gpu())) && fits;
+  if (tb_ && block) {
+    if (cfg_.kernel2.empty() || cfg_.kernel2 == "auto") kspec2_.kind = KernelSpec::TBR;
+    if (kspec2_.kind != KernelSpec::TBR)
+      throw UsageError("temporal blocking with y/z neighbours needs a register-ring kernel (--kernel2 trK)");
+  }
   K_ = tb_ ? K : 1;
-  halo_depth_ = tb_ && dims[0] > 1 ? K : 1;
-  // overlapped sweeps need a non-empty interior between the boundary slabs
-  tb_overlap_ = tb_ && dims[0] > 1 && overlap_ && min_n0 >= 2 * K + 1;
+  for (int a = 0; a < 3; ++a) hd_[a] = tb_ && dims[a] > 1 ? K : 1;
+  halo_depth_ = hd_[0];
+  ordered_halo_ = tb_ && block;
+  // overlapped sweeps (x slabs only) need a non-empty interior between the
+  // boundary slabs; block decompositions exchange first, then sweep
+  tb_overlap_ = tb_ && dims[0] > 1 && !block && overlap_ && min_n0 >= 2 * K + 1;
   // lagged convergence check (third buffer, two residual-slot banks) keeps
   // the all-reduce + check off the critical path of the overlapped sweeps
   {
@@ -178,7 +193,7 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   for (int r : comm_->local_ranks()) {
     Local l;
     l.sd = dec_.subs[r];
-    l.L = Layout::make(l.sd.n, (int64_t)esize_, halo_depth_);
+    l.L = Layout::make(l.sd.n, (int64_t)esize_, hd_[0], hd_[1], hd_[2]);
     for (int b = 0; b < nbuf_; ++b) l.field[b] = be_->alloc(l.L.bytes());
     for (int a = 0; a < 3; ++a) {
       l.owned.lo[a] = 0;
@@ -188,6 +203,14 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     const bool lo = l.sd.has_neighbor(Face::Left), hi = l.sd.has_neighbor(Face::Right);
     l.ux[0] = lo ? -(K_ - 1) : 0;
     l.ux[1] = l.sd.n[0] + (hi ? K_ - 1 : 0);
+    // y / z update ranges reach into deep halos only where there is one
+    for (int a = 1; a < 3; ++a) {
+      int64_t* u = a == 1 ? l.uy : l.uz;
+      const bool nlo = l.sd.has_neighbor(static_cast<Face>(2 * a));
+      const bool nhi = l.sd.has_neighbor(static_cast<Face>(2 * a + 1));
+      u[0] = nlo && hd_[a] > 1 ? -(K_ - 1) : 0;
+      u[1] = l.sd.n[a] + (nhi && hd_[a] > 1 ? K_ - 1 : 0);
+    }
     l.tb_interior = l.owned;
     if (tb_overlap_) {
       l.tb_interior.lo[0] = lo ? K_ : 0;
@@ -254,11 +277,22 @@ void Solver::setup_faces() {
         io.send_box.lo[b] = io.recv_box.lo[b] = 0;
         io.send_box.hi[b] = io.recv_box.hi[b] = l.sd.n[b];
       }
-      const int64_t dep = a == 0 ? halo_depth_ : 1;
+      const int64_t dep = hd_[a];
       io.send_box.lo[a] = side ? l.sd.n[a] - dep : 0;
       io.send_box.hi[a] = io.send_box.lo[a] + dep;
       io.recv_box.lo[a] = side ? l.sd.n[a] : -dep;
       io.recv_box.hi[a] = io.recv_box.lo[a] + dep;
+      if (ordered_halo_) {
+        // axis-ordered exchange (x, then y, then z): a face of axis a also
+        // carries the deep ghosts of the axes before it, which the earlier
+        // phases have filled, so edges and corners arrive in the right order
+        for (int b = 0; b < a; ++b) {
+          const int64_t elo = l.sd.has_neighbor(static_cast<Face>(2 * b)) ? hd_[b] : 0;
+          const int64_t ehi = l.sd.has_neighbor(static_cast<Face>(2 * b + 1)) ? hd_[b] : 0;
+          io.send_box.lo[b] = io.recv_box.lo[b] = -elo;
+          io.send_box.hi[b] = io.recv_box.hi[b] = l.sd.n[b] + ehi;
+        }
+      }
       if (comm_->all_local()) {
         for (std::size_t q = 0; q < local_.size(); ++q)
           if (local_[q].sd.rank == io.peer) io.peer_local = (int)q;
@@ -357,9 +391,22 @@ void Solver::initialize() {
 void Solver::enqueue_halo(int p, StreamId s) {
   // p = buffer index whose faces / ghosts are exchanged
   be_->range_push("halo");
+  // one phase per axis when edges / corners must follow the faces
+  // (ordered_halo_), else all faces at once
+  const int nphase = ordered_halo_ ? 3 : 1;
+  for (int ph = 0; ph < nphase; ++ph) {
+    auto in_phase = [&](const FaceIO& io) { return !ordered_halo_ || face_axis(io.face) == ph; };
+    enqueue_halo_phase(p, s, in_phase);
+  }
+  be_->range_pop();
+}
+
+template <typename Pred>
+void Solver::enqueue_halo_phase(int p, StreamId s, Pred in_phase) {
   if (comm_->all_local()) {
     for (auto& l : local_)
       for (auto& io : l.faces) {
+        if (!in_phase(io)) continue;
         const Local& nb = local_[io.peer_local];
         const Box* src = nullptr;
         for (auto& nio : nb.faces)
@@ -372,6 +419,7 @@ void Solver::enqueue_halo(int p, StreamId s) {
     for (auto& l : local_) {
       char* base = static_cast<char*>(l.field[p]);
       for (auto& io : l.faces) {
+        if (!in_phase(io)) continue;
         if (!io.contiguous) be_->pack_box(dt_, l.field[p], l.L, io.send_box, io.sendbuf, s);
         Transfer snd, rcv;
         snd.src_rank = l.sd.rank;
@@ -386,12 +434,11 @@ void Solver::enqueue_halo(int p, StreamId s) {
         xs.push_back(rcv);
       }
     }
-    comm_->exchange(xs, *be_, s);
+    if (!xs.empty()) comm_->exchange(xs, *be_, s);
     for (auto& l : local_)
       for (auto& io : l.faces)
-        if (!io.contiguous) be_->unpack_box(dt_, l.field[p], l.L, io.recv_box, io.recvbuf, s);
+        if (in_phase(io) && !io.contiguous) be_->unpack_box(dt_, l.field[p], l.L, io.recv_box, io.recvbuf, s);
   }
-  be_->range_pop();
 }
 
 static bool trace_on() {
@@ -511,6 +558,10 @@ void Solver::enqueue_multi(int bi) {
     sp.slot = slot0;
     sp.ux[0] = l.ux[0];
     sp.ux[1] = l.ux[1];
+    for (int e = 0; e < 2; ++e) {
+      sp.uy[e] = l.uy[e];
+      sp.uz[e] = l.uz[e];
+    }
     return sp;
   };
   auto reduce_and_check = [&](StreamId s) {
@@ -609,8 +660,11 @@ void Solver::finalize_converged(int64_t c) {
         sp.L = l.L;
         sp.box = l.owned;
         const int64_t w = m - j;
-        if (l.sd.has_neighbor(Face::Left)) sp.box.lo[0] -= w;
-        if (l.sd.has_neighbor(Face::Right)) sp.box.hi[0] += w;
+        for (int a = 0; a < 3; ++a) {
+          if (hd_[a] <= 1) continue;
+          if (l.sd.has_neighbor(static_cast<Face>(2 * a))) sp.box.lo[a] -= w;
+          if (l.sd.has_neighbor(static_cast<Face>(2 * a + 1))) sp.box.hi[a] += w;
+        }
         for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
         sp.state = nullptr;  // forced: ignores the done flag, no residual
         be_->stencil(dt_, sp, kspec_, kCompute);

@@ -156,6 +156,7 @@ class Solver {
     Box tb_interior;
     std::vector<Box> tb_boundary;
     int64_t ux[2] = {0, -1};
+    int64_t uy[2] = {0, -1}, uz[2] = {0, -1};  // y / z update ranges (deep y / z halos)
   };
 
   void setup_faces();
@@ -164,6 +165,8 @@ class Solver {
   // K iterations in one temporally blocked sweep from buffer bi
   void enqueue_multi(int bi);
   void enqueue_halo(int bi, StreamId s);
+  template <typename Pred>
+  void enqueue_halo_phase(int bi, StreamId s, Pred in_phase);
   void join_pipeline();      // every stream waits for every pipeline event
   bool multi_stream() const { return tb_ ? tb_overlap_ : overlap_; }
   // buffer holding T^{issued_}; a step or a K-step sweep reads cur() and
@@ -191,6 +194,8 @@ class Solver {
   bool overlap_ = true;
   bool tb_overlap_ = false;   // sweeps: interior || (deep halo -> boundary slabs)
   int halo_depth_ = 1;        // x-face halo planes (K with temporal blocking)
+  int64_t hd_[3] = {1, 1, 1}; // halo depth per axis (K on split axes with temporal blocking)
+  bool ordered_halo_ = false; // axis-ordered exchange filling edges / corners (deep y / z halos)
   int last_kind_ = 0;         // 1 = single step, 2 = pair: last enqueued schedule
   DType dt_;
   std::size_t esize_;

@@ -245,3 +245,35 @@ def test_sweep_nan_faults(h3d, gpu, kernel2):
     s.native.inject(0, 20, 18, 22, float("nan"))
     r = s.run()
     assert r["fault"] and not r["converged"], r
+
+
+@pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2), (2, 1, 3), (1, 3, 1), (1, 1, 2)])
+@pytest.mark.parametrize("kernel2,dtype", [("tr3", "fp64"), ("tr2", "fp64"), ("tr4", "fp64"),
+                                           ("tr3:1:6:1:8:0:3", "fp64"), ("tr3", "fp32"), ("tr4:1:4:1:8:0:3", "fp32")])
+def test_block_decomposition_ring_kernel_gpu(h3d, gpu, dims, kernel2, dtype):
+    """Deep y / z halos (axis-ordered exchange with edges and corners) and the
+    ring kernel's y / z update ranges: virtual-rank block decompositions on
+    the GPU equal the single-domain single-step run bit for bit."""
+    n = (45, 61, 150)
+    P = dims[0] * dims[1] * dims[2]
+    a = h3d.HeatSolver(n, 29, 0.0, dtype=dtype, backend="hip", virtual_ranks=P, decomp=dims,
+                       extra_args=["--kernel2", kernel2])
+    b = h3d.HeatSolver(n, 29, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
+    assert a.native.temporal_blocking and a.native.kernel_name.startswith(kernel2.split(":")[0])
+    ra, rb = a.run(), b.run()
+    assert ra["iterations"] == rb["iterations"] == 29
+    assert ra["last_residual"] == rb["last_residual"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2)])
+def test_block_decomposition_ring_kernel_rollback_gpu(h3d, gpu, dims):
+    P = dims[0] * dims[1] * dims[2]
+    for eps in (1e-3, 9e-4, 8e-4):
+        a = h3d.HeatSolver((33, 33, 33), 10 ** 6, eps, backend="hip", virtual_ranks=P, decomp=dims,
+                           extra_args=["--check-every", "7"])
+        b = h3d.HeatSolver((33, 33, 33), 10 ** 6, eps, backend="hip", extra_args=["--temporal", "1"])
+        assert a.native.temporal_blocking
+        ra, rb = a.run(), b.run()
+        assert ra["conv_iter"] == rb["conv_iter"] and ra["converged"]
+        assert np.array_equal(a.gather(), b.gather()), (dims, eps)

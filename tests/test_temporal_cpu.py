@@ -79,9 +79,11 @@ def test_single_plane_slabs_fall_back(h3d):
     assert not s.native.temporal_blocking
 
 
-def test_block_decomposition_stays_single_step(h3d):
+def test_block_decomposition_uses_ring_kernel(h3d):
+    # y / z splits take temporal blocking too, with the register-ring kernel
     s = h3d.HeatSolver((17, 17, 17), 10, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1), extra_args=T2)
-    assert not s.native.temporal_blocking
+    assert s.native.temporal_blocking and s.native.temporal_steps == 2
+    assert s.native.kernel_name.startswith("tr2"), s.native.kernel_name
 
 
 def test_slab_pairs_verify_halos(h3d):
@@ -148,3 +150,51 @@ def test_lagged_check_uses_three_buffers(h3d, K, monkeypatch):
         assert ra["conv_iter"] == rb["conv_iter"] == rc["conv_iter"] and ra["converged"]
         ref = b.gather()
         assert np.array_equal(a.gather(), ref) and np.array_equal(c.gather(), ref), (K, eps)
+
+
+BLOCKS = [(2, 2, 1), (1, 2, 2), (2, 2, 2), (1, 1, 3), (3, 2, 1), (1, 3, 1)]
+
+
+@pytest.mark.parametrize("dims", BLOCKS)
+@pytest.mark.parametrize("K", [2, 3, 4])
+def test_block_decomposition_temporal_matches_single_step(h3d, dims, K):
+    """K-step sweeps with deep y / z halos (axis-ordered exchange filling the
+    edge and corner ghosts) reproduce the single-step solver bit for bit."""
+    n = (27, 25, 29)
+    P = dims[0] * dims[1] * dims[2]
+    a = h3d.HeatSolver(n, 23, 0.0, backend="cpu", virtual_ranks=P, decomp=dims,
+                       extra_args=["--temporal", str(K)])
+    b = h3d.HeatSolver(n, 23, 0.0, backend="cpu", extra_args=T1)
+    assert a.native.temporal_blocking and a.native.temporal_steps == K
+    ra, rb = a.run(), b.run()
+    assert ra["iterations"] == rb["iterations"] == 23
+    assert ra["last_residual"] == rb["last_residual"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2)])
+@pytest.mark.parametrize("K", [3, 4])
+def test_block_decomposition_temporal_rollback(h3d, dims, K):
+    # converged iteration lands at every offset inside a K-sweep
+    P = dims[0] * dims[1] * dims[2]
+    for eps in (1e-3, 9e-4, 8e-4, 7e-4):
+        a = h3d.HeatSolver((25, 25, 25), 10 ** 6, eps, backend="cpu", virtual_ranks=P, decomp=dims,
+                           extra_args=["--temporal", str(K), "--check-every", "5"])
+        b = h3d.HeatSolver((25, 25, 25), 10 ** 6, eps, backend="cpu", extra_args=T1)
+        ra, rb = a.run(), b.run()
+        assert ra["conv_iter"] == rb["conv_iter"] and ra["converged"]
+        assert np.array_equal(a.gather(), b.gather()), (dims, K, eps)
+
+
+def test_block_decomposition_verify_halos(h3d):
+    s = h3d.HeatSolver((21, 23, 25), 12, 0.0, backend="cpu", virtual_ranks=8, decomp=(2, 2, 2),
+                       extra_args=["--temporal", "3"])
+    s.run()
+    assert s.native.verify_halos() == 0
+
+
+def test_block_decomposition_too_thin_falls_back(h3d):
+    # 5 interior points over 3 ranks along y: some subdomain has < K = 3 rows
+    s = h3d.HeatSolver((17, 7, 17), 10, 0.0, backend="cpu", virtual_ranks=3, decomp=(1, 3, 1),
+                       extra_args=["--temporal", "3"])
+    assert not s.native.temporal_blocking
