@@ -90,11 +90,13 @@ KernelSpec KernelSpec::resolved(DType t) const {
       def(r.WY, f64 ? 16 : 8);
       def(r.NT, 1);  // prefetch depth
       break;
-    case TBR:  // 7th field = T^n ring size.  fp64: K = 2 32 x 128 tiles, K = 3
+    case TBR:  // 7th field = T^n ring size.  fp64: K = 2 64 x 64 tiles, K = 3
                // 48 x 64, K >= 4 32 x 64 (8 waves); fp32: 32 x 128.  All
-               // without register spills (launch_tbr refuses spilling variants).
-      def(r.V, f64 ? (K == 2 ? 2 : 1) : 2);
-      def(r.R, f64 ? (K == 2 ? 2 : K == 3 ? 3 : 4) : 4);
+               // without register spills (launch_tbr refuses spilling variants;
+               // the former K = 2 fp64 default 2:2:1:16 spills since the y / z
+               // update ranges).
+      def(r.V, f64 ? 1 : 2);
+      def(r.R, f64 ? (K == 3 ? 3 : 4) : 4);
       def(r.WZ, 1);
       def(r.WY, f64 ? (K <= 3 ? 16 : 8) : 8);
       def(r.NT, 3);
