@@ -541,14 +541,28 @@ void Solver::enqueue_iteration(int p, int bi) {
 // under sweep q+1, whose residuals go to the other slot bank; if sweep q
 // converged, q+1 was speculative (its output buffer is not q's input) and
 // q+2 onwards are no-ops.  Exchanged values stay bitwise identical.
-void Solver::enqueue_multi(int bi) {
-  H3D_TRACE("sweep" << K_ << " issued=" << issued_ << " buf=" << bi << (capturing_ ? " (capturing)" : ""));
+void Solver::enqueue_multi(int bi, int Kp) {
+  // Kp < K_: a partial sweep of Kp steps (the remainder of a step count that
+  // is not a multiple of K_), same schedule and buffers, ring kernel of depth Kp
+  if (Kp <= 0) Kp = K_;
+  H3D_TRACE("sweep" << Kp << " issued=" << issued_ << " buf=" << bi << (capturing_ ? " (capturing)" : ""));
   HEAT3D_CHECK(tb_, "temporal blocking not enabled for this decomposition");
   if (last_kind_ != 2) join_pipeline();
   last_kind_ = 2;
   // lagged schedule: events and residual slots alternate by sweep parity
   const int q = lag_ ? (int)(nsweep_ & 1) : bi;
   const int slot0 = lag_ ? q * K_ : 0;
+  KernelSpec ks = kspec2_;
+  if (Kp != K_) {
+    ks = KernelSpec();
+    ks.kind = KernelSpec::TBR;
+    ks.K = Kp;
+  }
+  // update ranges reach Kp - 1 (not K_ - 1) points into the deep halos
+  auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
+    o[0] = u[0] < 0 ? -(Kp - 1) : u[0];
+    o[1] = u[1] > n ? n + Kp - 1 : u[1];
+  };
   auto params = [&](Local& l, const Box& b) {
     StencilParams sp;
     sp.in = l.field[bi];
@@ -558,27 +572,24 @@ void Solver::enqueue_multi(int bi) {
     for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
     sp.state = dstate_;
     sp.slot = slot0;
-    sp.ux[0] = l.ux[0];
-    sp.ux[1] = l.ux[1];
-    for (int e = 0; e < 2; ++e) {
-      sp.uy[e] = l.uy[e];
-      sp.uz[e] = l.uz[e];
-    }
+    shrink(l.ux, l.sd.n[0], sp.ux);
+    shrink(l.uy, l.sd.n[1], sp.uy);
+    shrink(l.uz, l.sd.n[2], sp.uz);
     return sp;
   };
   auto reduce_and_check = [&](StreamId s) {
     if (!comm_->all_local() && comm_->size() > 1)
-      comm_->allreduce(&dstate_->residual[slot0], K_, RedType::U64, RedOp::Max, *be_, s);
+      comm_->allreduce(&dstate_->residual[slot0], Kp, RedType::U64, RedOp::Max, *be_, s);
     else if (fake_allreduce_us_ > 0)
       be_->delay(fake_allreduce_us_, s);  // single-GPU stand-in for the RCCL latency
-    be_->check_convergence(dstate_, slot0, s, K_);
+    be_->check_convergence(dstate_, slot0, s, Kp);
   };
   if (!tb_overlap_) {
     ev_wait(kCompute, EV_CHK + 0);
     ev_wait(kCompute, EV_CHK + 1);
     if (has_halo_) enqueue_halo(bi, kCompute);
     be_->range_push("sweep");
-    for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), kspec2_, kCompute);
+    for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), ks, kCompute);
     be_->range_pop();
     reduce_and_check(kCompute);
     if (!capturing_) {
@@ -602,7 +613,7 @@ void Solver::enqueue_multi(int bi) {
   ev_wait(kCompute, EV_CHK + chk_prev);
   ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of our input
   be_->range_push("interior");
-  for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), kspec2_, kCompute);
+  for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), ks, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
   // [B] deep halo, then the boundary slabs
@@ -611,7 +622,7 @@ void Solver::enqueue_multi(int bi) {
   ev_wait(kComm, EV_CHK + chk_prev);
   be_->range_push("boundary");
   for (auto& l : local_)
-    for (const Box& b : l.tb_boundary) be_->stencil2(dt_, params(l, b), kspec2_, kComm);
+    for (const Box& b : l.tb_boundary) be_->stencil2(dt_, params(l, b), ks, kComm);
   be_->range_pop();
   ev_record(EV_BND + q, kComm);
   // [C] all residuals, all checks
@@ -797,12 +808,14 @@ void Solver::run_chunk(int64_t n) {
         continue;
       }
     }
-    if (tb_ && n >= K_ && !phase_timing_) {
-      record_segment(issued_, K_, cur());
-      enqueue_multi(cur());
-      issued_ += K_;
+    if (tb_ && n >= 2 && !phase_timing_) {
+      // a full sweep, or a partial one for a remainder of 2 .. K-1 steps
+      const int Kp = (int)std::min<int64_t>(n, K_);
+      record_segment(issued_, Kp, cur());
+      enqueue_multi(cur(), Kp);
+      issued_ += Kp;
       cur_ = nxt(cur_);
-      n -= K_;
+      n -= Kp;
       continue;
     }
     if (phase_timing_ && !tev_[0])

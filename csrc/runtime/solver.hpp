@@ -163,7 +163,7 @@ class Solver {
   // one single-step iteration: residual slot / event parity p, input buffer bi
   void enqueue_iteration(int p, int bi);
   // K iterations in one temporally blocked sweep from buffer bi
-  void enqueue_multi(int bi);
+  void enqueue_multi(int bi, int Kp = 0);
   void enqueue_halo(int bi, StreamId s);
   template <typename Pred>
   void enqueue_halo_phase(int bi, StreamId s, Pred in_phase);

@@ -198,3 +198,22 @@ def test_block_decomposition_too_thin_falls_back(h3d):
     s = h3d.HeatSolver((17, 7, 17), 10, 0.0, backend="cpu", virtual_ranks=3, decomp=(1, 3, 1),
                        extra_args=["--temporal", "3"])
     assert not s.native.temporal_blocking
+
+
+@pytest.mark.parametrize("K", [3, 4])
+@pytest.mark.parametrize("vr,dims", [(1, (1, 1, 1)), (3, (3, 1, 1)), (4, (2, 2, 1))])
+@pytest.mark.parametrize("iters", [2, 5, 11])
+def test_partial_sweep_remainders(h3d, K, vr, dims, iters):
+    """Step counts that are not a multiple of K end with a partial sweep of
+    2..K-1 steps (ring kernel of that depth) instead of single steps."""
+    n = (31, 23, 27)
+    a = h3d.HeatSolver(n, iters, 0.0, backend="cpu", virtual_ranks=vr, decomp=dims,
+                       extra_args=["--temporal", str(K)])
+    b = h3d.HeatSolver(n, iters, 0.0, backend="cpu", extra_args=T1)
+    a.initialize()
+    b.initialize()
+    a.step(iters)
+    b.step(iters)
+    sa, sb = a.native.state(), b.native.state()
+    assert sa["iter"] == sb["iter"] == iters and sa["last_residual"] == sb["last_residual"]
+    assert np.array_equal(a.gather(), b.gather())
