@@ -147,7 +147,8 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
     allst &= zst[v];
     if constexpr (!kColAcc)
 #pragma unroll
-      for (int s = 0; s < K; ++s) lres[s][v] = zin[v] && cp >= s && cp < TZ - s;
+      for (int s = 0; s < K; ++s)
+        lres[s][v] = zin[v] && cp >= s && cp < TZ - s && kk >= g.blo[2] - (K - 1 - s) && kk < g.bhi[2] + (K - 1 - s);
   }
   const int64_t wbase = g.origin + (int64_t)yb * sy + tkb;
   const Real* __restrict__ inw = in + wbase;
@@ -263,7 +264,11 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
             // padded steps past xlast compute planes beyond the sweep's box
             // widened by K-1-s (possibly from halo planes still being
             // exchanged): never counted
-            const bool rres = yin && xval && x <= xlast && rp >= s && rp < TYB - s;
+            // counted: valid inputs (tile-relative), and within the box
+            // widened by K-1-s — beyond it a stage-s value may come from
+            // held or still-arriving halo data (deep y halos)
+            const bool rres = yin && xval && x <= xlast && rp >= s && rp < TYB - s &&
+                              row >= g.blo[1] - (K - 1 - s) && row < g.bhi[1] + (K - 1 - s);
             const Real left = s == 0 ? readlane(ed[sC], r) : Real(0);
             const Real right = s == 0 ? readlane(ed[sC], 32 + r) : Real(0);
             const Real* ym = r == 0 ? lo : C[r > 0 ? r - 1 : 0];
@@ -340,7 +345,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
       nan_any |= (!kColAcc || zst[v]) && nan_seen[v];
 #pragma unroll
       for (int s = 0; s < K; ++s) {
-        const bool ok = !kColAcc || (s == K - 1 ? zst[v] : (zin[v] && cp >= s && cp < TZ - s));
+        const int kk = k + v;
+        const bool ok = !kColAcc || (s == K - 1 ? zst[v]
+                                                : (zin[v] && cp >= s && cp < TZ - s && kk >= g.blo[2] - (K - 1 - s) &&
+                                                   kk < g.bhi[2] + (K - 1 - s)));
         mm[s] = fmax(mm[s], ok ? m[s][v] : 0.0);
       }
     }

@@ -43,9 +43,9 @@ Box to_box(const std::array<int64_t, 6>& b) {
   return r;
 }
 
-Layout to_layout(const std::array<int64_t, 3>& n, int64_t esize, int64_t gx = 1) {
+Layout to_layout(const std::array<int64_t, 3>& n, int64_t esize, int64_t gx = 1, int64_t gy = 1, int64_t gz = 1) {
   int64_t nn[3] = {n[0], n[1], n[2]};
-  return Layout::make(nn, esize, gx);
+  return Layout::make(nn, esize, gx, gy, gz);
 }
 
 py::dict layout_dict(const Layout& L) {
@@ -215,8 +215,10 @@ PYBIND11_MODULE(_heat3d, m) {
     for (auto& b : shell) sl.append(tup(b));
     return py::make_tuple(tup(in), sl);
   });
-  m.def("layout", [](std::array<int64_t, 3> n, int64_t esize, int64_t gx) { return layout_dict(to_layout(n, esize, gx)); },
-        py::arg("n"), py::arg("esize"), py::arg("gx") = 1);
+  m.def("layout", [](std::array<int64_t, 3> n, int64_t esize, int64_t gx, int64_t gy, int64_t gz) {
+          return layout_dict(to_layout(n, esize, gx, gy, gz));
+        },
+        py::arg("n"), py::arg("esize"), py::arg("gx") = 1, py::arg("gy") = 1, py::arg("gz") = 1);
   m.def("boundary_value", [](int64_t i, int64_t j, int64_t k, std::array<int64_t, 3> N, std::array<double, 3> h) {
     int64_t n[3] = {N[0], N[1], N[2]};
     double hh[3] = {h[0], h[1], h[2]};
@@ -259,6 +261,24 @@ PYBIND11_MODULE(_heat3d, m) {
     p.ux[1] = ux[1];
     KernelSpec k = KernelSpec::parse(kernel);
     if (!k.multi_step()) throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 / tr2..tr6 kernel");
+    hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
+  });
+  // deep ghosts on every axis (block decompositions): g = (gx, gy, gz),
+  // u = update ranges (ux0, ux1, uy0, uy1, uz0, uz1)
+  hk.def("stencil_sweep3", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
+                              std::array<int64_t, 3> g, std::array<int64_t, 6> box, std::array<int64_t, 6> u,
+                              std::array<double, 3> D, int64_t state_ptr, int slot, const std::string& kernel,
+                              int64_t stream) {
+    DType t = dt_of(dt);
+    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
+    p.L = to_layout(n, (int64_t)dtype_size(t), g[0], g[1], g[2]);
+    for (int e = 0; e < 2; ++e) {
+      p.ux[e] = u[e];
+      p.uy[e] = u[2 + e];
+      p.uz[e] = u[4 + e];
+    }
+    KernelSpec k = KernelSpec::parse(kernel);
+    if (!k.multi_step()) throw UsageError("stencil_sweep3 needs a tr2..tr6 kernel");
     hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
   });
   hk.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
@@ -312,6 +332,23 @@ PYBIND11_MODULE(_heat3d, m) {
     p.ux[1] = ux[1];
     KernelSpec k = KernelSpec::parse(kernel);
     if (!k.multi_step()) throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 / tr2..tr6 kernel");
+    std::vector<char> s0(p.L.bytes()), s1(p.L.bytes());
+    py::gil_scoped_release nogil;
+    cpu::stencil_multi(t, p, k.K, k.kind == KernelSpec::TB2, s0.data(), s1.data());
+  });
+  ck.def("stencil_sweep3", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
+                              std::array<int64_t, 3> g, std::array<int64_t, 6> box, std::array<int64_t, 6> u,
+                              std::array<double, 3> D, int64_t state_ptr, int slot, const std::string& kernel) {
+    DType t = dt_of(dt);
+    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
+    p.L = to_layout(n, (int64_t)dtype_size(t), g[0], g[1], g[2]);
+    for (int e = 0; e < 2; ++e) {
+      p.ux[e] = u[e];
+      p.uy[e] = u[2 + e];
+      p.uz[e] = u[4 + e];
+    }
+    KernelSpec k = KernelSpec::parse(kernel);
+    if (!k.multi_step()) throw UsageError("stencil_sweep3 needs a tr2..tr6 kernel");
     std::vector<char> s0(p.L.bytes()), s1(p.L.bytes());
     py::gil_scoped_release nogil;
     cpu::stencil_multi(t, p, k.K, k.kind == KernelSpec::TB2, s0.data(), s1.data());

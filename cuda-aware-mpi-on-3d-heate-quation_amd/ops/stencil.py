@@ -22,13 +22,15 @@ _DT = {torch.float64: "fp64", torch.float32: "fp32"}
 class PaddedField:
     """One subdomain field in the native padded layout."""
 
-    def __init__(self, n: Sequence[int], dtype=torch.float64, device="cpu", gx: int = 1):
+    def __init__(self, n: Sequence[int], dtype=torch.float64, device="cpu", gx: int = 1, gy: int = 1, gz: int = 1):
         if dtype not in _DT:
             raise TypeError(f"unsupported dtype {dtype}")
         self.n = tuple(int(v) for v in n)
         self.dtype = dtype
         self.gx = int(gx)  # ghost planes per x side (deep halos of the K-step slab schedule)
-        self.layout = native().layout(list(self.n), torch.tensor([], dtype=dtype).element_size(), self.gx)
+        self.gy, self.gz = int(gy), int(gz)  # ghost rows / columns (deep y / z halos of block splits)
+        self.layout = native().layout(list(self.n), torch.tensor([], dtype=dtype).element_size(), self.gx,
+                                      self.gy, self.gz)
         self.flat = torch.zeros(self.layout["elems"], dtype=dtype, device=device)
 
     @property
@@ -44,6 +46,13 @@ class PaddedField:
         L = self.layout
         off = L["origin"] - L["sx"] - L["sy"] - 1
         shape = tuple(v + 2 for v in self.n)
+        return self.flat.as_strided(shape, (L["sx"], L["sy"], 1), off)
+
+    def deep3(self) -> torch.Tensor:
+        """View (n0+2gx, n1+2gy, n2+2gz): every ghost layer on every axis."""
+        L = self.layout
+        off = L["origin"] - self.gx * L["sx"] - self.gy * L["sy"] - self.gz
+        shape = (self.n[0] + 2 * self.gx, self.n[1] + 2 * self.gy, self.n[2] + 2 * self.gz)
         return self.flat.as_strided(shape, (L["sx"], L["sy"], 1), off)
 
     def deep(self) -> torch.Tensor:
@@ -139,6 +148,27 @@ def sweep(src: PaddedField, dst: PaddedField, D: Sequence[float], box: Sequence[
         native().hip.stencil_sweep(*args, _stream_ptr(src.flat))
     else:
         native().cpu.stencil_sweep(*args)
+
+
+def sweep3(src: PaddedField, dst: PaddedField, D: Sequence[float], box: Sequence[int], u: Sequence[int],
+           kernel: str = "tr3", state: Optional[torch.Tensor] = None, slot: int = 0) -> None:
+    """K-step sweep with deep ghosts on every axis (the block-decomposition
+    schedule): ``u`` = (ux0, ux1, uy0, uy1, uz0, uz1) are the update ranges of
+    the intermediate steps.  GPU tensors run the ring kernel, CPU tensors the
+    K-single-steps definition."""
+    if src.layout != dst.layout or src.dtype != dst.dtype or src.device != dst.device:
+        raise ValueError("src and dst must share layout, dtype and device")
+    sptr = 0
+    if state is not None:
+        if state.device != src.device or state.numel() * state.element_size() < native().DEVICE_STATE_BYTES:
+            raise ValueError("state tensor too small or on the wrong device")
+        sptr = state.data_ptr()
+    args = (src.dt, src.data_ptr(), dst.data_ptr(), list(src.n), [src.gx, src.gy, src.gz], list(box), list(u),
+            list(D), sptr, slot, kernel)
+    if src.device.type == "cuda":
+        native().hip.stencil_sweep3(*args, _stream_ptr(src.flat))
+    else:
+        native().cpu.stencil_sweep3(*args)
 
 
 def init_field(f: PaddedField, gstart: Sequence[int], N: Sequence[int], h: Sequence[float]) -> None:

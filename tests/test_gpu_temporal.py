@@ -277,3 +277,51 @@ def test_block_decomposition_ring_kernel_rollback_gpu(h3d, gpu, dims):
         ra, rb = a.run(), b.run()
         assert ra["conv_iter"] == rb["conv_iter"] and ra["converged"]
         assert np.array_equal(a.gather(), b.gather()), (dims, eps)
+
+
+def _deep3_random(ops, n, g, dtype, seed):
+    gen = torch.Generator().manual_seed(seed)
+    f = ops.PaddedField(n, dtype=dtype, gx=g, gy=g, gz=g)
+    f.deep3().copy_(torch.rand(f.deep3().shape, generator=gen, dtype=torch.float64).to(dtype))
+    return f
+
+
+@pytest.mark.parametrize("kernel", ["tr2", "tr3", "tr4", "tr3:1:6:1:8:0:3", "tr3:1:3:1:16:0:3:1"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("box,sides", [((0, 12, 0, 50, 0, 140), "lo"), ((0, 12, 0, 50, 0, 140), "hi"),
+                                       ((0, 12, 0, 50, 0, 140), "both"), ((0, 12, 4, 46, 0, 140), "both"),
+                                       ((3, 9, 0, 4, 0, 140), "both"), ((0, 12, 46, 50, 5, 135), "both"),
+                                       ((0, 12, 0, 50, 136, 140), "both"), ((2, 10, 3, 47, 0, 4), "both")])
+def test_sweep_deep_yz_halo_matches_cpu(h3d, gpu, kernel, dtype, box, sides):
+    """Deep ghosts on every axis (block decompositions): the ring kernel's
+    y / z update ranges and its residual (only the box widened by K-1-s
+    counts at stage s) equal the CPU K-single-steps definition on random
+    fields, for thin / partial boxes such as the interior/boundary pieces."""
+    ops = h3d.ops
+    head = kernel.split(":")[0]
+    K = int(head[2])
+    n = (12, 50, 140)
+    lo, hi = sides in ("lo", "both"), sides in ("hi", "both")
+    u = []
+    for a in range(3):
+        u += [-(K - 1) if lo else 0, n[a] + (K - 1 if hi else 0)]
+    D = (0.06, 0.05, 0.04)
+    src = _deep3_random(ops, n, K, dtype, 11)
+    want = ops.PaddedField(n, dtype=dtype, gx=K, gy=K, gz=K)
+    want.flat.fill_(-5.0)
+    st_c = ops.new_state("cpu")
+    ops.sweep3(src, want, D, box, u, kernel=kernel, state=st_c)
+    dsrc = ops.PaddedField(n, dtype=dtype, device=gpu, gx=K, gy=K, gz=K)
+    dsrc.flat.copy_(src.flat)
+    got = ops.PaddedField(n, dtype=dtype, device=gpu, gx=K, gy=K, gz=K)
+    got.flat.fill_(-5.0)
+    st_g = ops.new_state(gpu)
+    ops.sweep3(dsrc, got, D, box, u, kernel=kernel, state=st_g)
+    torch.cuda.synchronize()
+    x0, x1, y0, y1, z0, z1 = box
+    a = got.owned().cpu()[x0:x1, y0:y1, z0:z1]
+    b = want.owned()[x0:x1, y0:y1, z0:z1]
+    assert torch.equal(a, b), f"{kernel} {box} {sides}: max diff {(a - b).abs().max().item()}"
+    res_c = [ops.residual_from_state(st_c, s) for s in range(K)]
+    res_g = [ops.residual_from_state(st_g, s) for s in range(K)]
+    assert res_c == res_g, (res_c, res_g)
