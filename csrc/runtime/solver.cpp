@@ -180,9 +180,13 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   for (int a = 0; a < 3; ++a) hd_[a] = tb_ && dims[a] > 1 ? K : 1;
   halo_depth_ = hd_[0];
   ordered_halo_ = tb_ && block;
-  // overlapped sweeps (x slabs only) need a non-empty interior between the
-  // boundary slabs; block decompositions exchange first, then sweep
-  tb_overlap_ = tb_ && dims[0] > 1 && !block && overlap_ && min_n0 >= 2 * K + 1;
+  // overlapped sweeps need a non-empty interior between the boundary layers
+  // of every split axis; otherwise exchange first, then sweep
+  bool thick = true;
+  for (int a = 0; a < 3; ++a) thick &= dims[a] == 1 || min_n[a] >= 2 * K + 1;
+  const char* ebo = std::getenv("HEAT3D_BLOCK_OVERLAP");
+  const bool block_overlap = !(ebo && ebo[0] == '0');
+  tb_overlap_ = tb_ && dims[0] * dims[1] * dims[2] > 1 && overlap_ && thick && (!block || block_overlap);
   // lagged convergence check (third buffer, two residual-slot banks) keeps
   // the all-reduce + check off the critical path of the overlapped sweeps
   {
@@ -215,15 +219,30 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     }
     l.tb_interior = l.owned;
     if (tb_overlap_) {
-      l.tb_interior.lo[0] = lo ? K_ : 0;
-      l.tb_interior.hi[0] = l.sd.n[0] - (hi ? K_ : 0);
-      for (int side = 0; side < 2; ++side) {
-        if (!(side ? hi : lo)) continue;
-        Box b = l.owned;
-        b.lo[0] = side ? l.sd.n[0] - K_ : 0;
-        b.hi[0] = b.lo[0] + K_;
-        l.tb_boundary.push_back(b);
+      // interior: the owned box minus a K-thick layer on every face with a
+      // neighbour (its K-step update reads no ghost).  Boundary pieces, an
+      // onion: the K-thick layers of axis a span the interior range of the
+      // axes before a and the full range of the axes after it — disjoint,
+      // and together with the interior they tile the owned box.
+      bool nb[3][2];
+      for (int a = 0; a < 3; ++a)
+        for (int e = 0; e < 2; ++e) nb[a][e] = hd_[a] > 1 && l.sd.has_neighbor(static_cast<Face>(2 * a + e));
+      for (int a = 0; a < 3; ++a) {
+        if (nb[a][0]) l.tb_interior.lo[a] = K_;
+        if (nb[a][1]) l.tb_interior.hi[a] = l.sd.n[a] - K_;
       }
+      for (int a = 0; a < 3; ++a)
+        for (int side = 0; side < 2; ++side) {
+          if (!nb[a][side]) continue;
+          Box b = l.owned;
+          for (int c = 0; c < a; ++c) {
+            b.lo[c] = l.tb_interior.lo[c];
+            b.hi[c] = l.tb_interior.hi[c];
+          }
+          b.lo[a] = side ? l.sd.n[a] - K_ : 0;
+          b.hi[a] = b.lo[a] + K_;
+          l.tb_boundary.push_back(b);
+        }
     }
     local_.push_back(l);
   }

@@ -217,3 +217,23 @@ def test_partial_sweep_remainders(h3d, K, vr, dims, iters):
     sa, sb = a.native.state(), b.native.state()
     assert sa["iter"] == sb["iter"] == iters and sa["last_residual"] == sb["last_residual"]
     assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2), (2, 1, 3)])
+def test_block_overlap_matches_exchange_first(h3d, dims, monkeypatch):
+    """Overlapped block sweeps (interior || axis-ordered halo -> onion of
+    boundary pieces, lagged check on three buffers) equal the exchange-first
+    schedule (HEAT3D_BLOCK_OVERLAP=0) bit for bit, converged or not."""
+    P = dims[0] * dims[1] * dims[2]
+    n = (31, 29, 33)
+    for eps in (0.0, 8e-4):
+        a = h3d.HeatSolver(n, 10 ** 6 if eps else 25, eps, backend="cpu", virtual_ranks=P, decomp=dims,
+                           extra_args=["--temporal", "3", "--check-every", "5"])
+        monkeypatch.setenv("HEAT3D_BLOCK_OVERLAP", "0")
+        b = h3d.HeatSolver(n, 10 ** 6 if eps else 25, eps, backend="cpu", virtual_ranks=P, decomp=dims,
+                           extra_args=["--temporal", "3", "--check-every", "5"])
+        monkeypatch.delenv("HEAT3D_BLOCK_OVERLAP")
+        assert a.native.field_buffers == 3 and b.native.field_buffers == 2
+        ra, rb = a.run(), b.run()
+        assert ra["conv_iter"] == rb["conv_iter"] and ra["last_residual"] == rb["last_residual"]
+        assert np.array_equal(a.gather(), b.gather())
