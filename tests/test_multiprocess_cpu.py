@@ -76,3 +76,18 @@ def test_native_socket_temporal_slabs(h3d, tmp_path, world):
     r1 = single.run()
     assert int(open(tmp_path / "result.txt").read().split()[0]) == r1["conv_iter"]
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
+
+
+@pytest.mark.parametrize("world,decomp", [(4, (2, 2, 1)), (4, (1, 2, 2)), (8, (2, 2, 2))])
+def test_native_socket_temporal_blocks(h3d, tmp_path, world, decomp):
+    """3-step temporal blocking across processes with y / z splits: the
+    axis-ordered deep halo (pack -> exchange -> unpack per axis), overlapped
+    boundary pieces, the lagged all-reduce of the residual slots — the
+    non-local code path RCCL takes on a multi-GPU node — over the socket
+    transport, bitwise equal to the single-process single-step solve."""
+    n, eps = 27, 1e-4
+    _spawn(native_socket_worker, world, str(tmp_path), n, eps, decomp, "fp64", ["--temporal", "3"])
+    single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", extra_args=["--temporal", "1"])
+    r1 = single.run()
+    assert int(open(tmp_path / "result.txt").read().split()[0]) == r1["conv_iter"]
+    assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
