@@ -237,3 +237,24 @@ def test_block_overlap_matches_exchange_first(h3d, dims, monkeypatch):
         ra, rb = a.run(), b.run()
         assert ra["conv_iter"] == rb["conv_iter"] and ra["last_residual"] == rb["last_residual"]
         assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("dims_a,dims_b", [((2, 2, 2), (1, 1, 1)), ((1, 1, 1), (2, 2, 1)), ((3, 1, 1), (1, 2, 2))])
+def test_checkpoint_restart_across_temporal_decompositions(h3d, tmp_path, dims_a, dims_b):
+    """A checkpoint written by a temporally blocked run (three buffers when
+    overlapped) restarts on any other decomposition and finishes at the same
+    iteration with the same field as an uninterrupted single-step solve."""
+    n, eps = 25, 1e-4
+    full = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", extra_args=T1)
+    rf = full.run()
+    Pa = dims_a[0] * dims_a[1] * dims_a[2]
+    Pb = dims_b[0] * dims_b[1] * dims_b[2]
+    a = h3d.HeatSolver((n, n, n), 301, eps, backend="cpu", virtual_ranks=Pa, decomp=dims_a,
+                       extra_args=["--temporal", "3"])
+    a.run()
+    a.save_checkpoint(str(tmp_path / "ck"))
+    b = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", virtual_ranks=Pb, decomp=dims_b,
+                       extra_args=["--temporal", "3", "--restart", str(tmp_path / "ck")])
+    rb = b.run()
+    assert rb["conv_iter"] == rf["conv_iter"]
+    assert np.array_equal(b.gather(), full.gather())
