@@ -112,15 +112,18 @@ def test_cli_multiprocess_socket(heat3d_bin, tmp_path):
     assert zones == 2
 
 
-@pytest.mark.parametrize("gpus,decomp", [(2, None), (4, "1x2x2"), (3, None)])
-def test_threads_per_rank_cli(heat3d_bin, tmp_path, gpus, decomp):
+@pytest.mark.parametrize("gpus,decomp,temporal", [(2, None, "0"), (4, "1x2x2", "0"), (3, None, "0"),
+                                                   (2, None, "3"), (4, "2x2x1", "3")])
+def test_threads_per_rank_cli(heat3d_bin, tmp_path, gpus, decomp, temporal):
     """--gpus N: N ranks in one process, one host thread each (the
     ncclCommInitAll-style runtime; TCP sockets between the threads on the CPU
-    backend).  Same report and checkpoint as the single-rank run."""
+    backend).  Same report and checkpoint as the single-rank run, also with
+    K-step temporal blocking (x slabs and y/z blocks across threads)."""
     base = ["23", "23", "23", "100000", "1e-4", "--backend", "cpu", "--output", "none"]
     one = run_cli(base + ["--checkpoint-every", "64", "--checkpoint-dir", "c1", "--json-out", "a.json"], tmp_path)
     assert one.returncode == 0, one.stderr
-    args = base + ["--gpus", str(gpus), "--checkpoint-every", "64", "--checkpoint-dir", "cn", "--json-out", "b.json"]
+    args = base + ["--gpus", str(gpus), "--checkpoint-every", "64", "--checkpoint-dir", "cn", "--json-out", "b.json",
+                   "--temporal", temporal]
     if decomp:
         args += ["--decomp", decomp]
     many = run_cli(args, tmp_path, env={"HEAT3D_BOOTSTRAP_PORT": str(free_port())})
