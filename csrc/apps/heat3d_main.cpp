@@ -27,6 +27,13 @@ using namespace heat3d;
 
 // --scheme reference: the reference's own decomposition, emulated in-process
 // (SURVEY.md App. B.3b); report lines as the reference printed them.
+// Single-step-equivalent HBM traffic (read + write of every point per
+// iteration, 2 * sizeof(Real) bytes): comparable with the copy bandwidth;
+// temporally blocked sweeps move less, so this can exceed the HBM rate.
+static double eff_tbps(double glups, heat3d::DType t) {
+  return glups * 2.0 * (double)heat3d::dtype_size(t) / 1e3;
+}
+
 static int run_reference_scheme(const Config& cfg) {
   const int P = cfg.virtual_ranks;
   std::array<int, 3> dims = cfg.decomp;
@@ -87,11 +94,11 @@ static int drive(const Config& cfg, Solver& solver) {
     if (!cfg.compat) {
       const auto& d = solver.decomposition();
       std::printf("heat3d: backend=%s comm=%s ranks=%d dims=%dx%dx%d dtype=%s kernel=%s "
-                  "iterations=%lld issued=%lld GLUPS=%.3f norm=%.6e last_residual=%.6e\n",
+                  "iterations=%lld issued=%lld GLUPS=%.3f eff_TBps=%.3f norm=%.6e last_residual=%.6e\n",
                   solver.backend().name(), solver.comm().name(), solver.comm().size(),
                   d.topo.dims[0], d.topo.dims[1], d.topo.dims[2], dtype_name(cfg.dtype),
                   solver.kernel_name().c_str(), (long long)r.iterations, (long long)r.issued,
-                  r.glups, r.norm, r.last_residual);
+                  r.glups, eff_tbps(r.glups, cfg.dtype), r.norm, r.last_residual);
     }
     if (cfg.timers) {
       std::printf("heat3d: phase timing (ms/iteration, synchronised):");
@@ -127,6 +134,7 @@ static int drive(const Config& cfg, Solver& solver) {
     j.set("issued", (int64_t)r.issued);
     j.set("seconds", r.seconds);
     j.set("glups", r.glups);
+    j.set("effective_tbps", eff_tbps(r.glups, cfg.dtype));
     j.set("norm", r.norm);
     j.set("last_residual", r.last_residual);
     j.set("error_percent", 100.0 * gerr);
