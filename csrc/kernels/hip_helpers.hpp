@@ -153,5 +153,17 @@ int device_slots(const void* kernel, int block);
 // x-segment length for an x-marching kernel with `halo` extra planes per segment.
 int choose_segment(int64_t nx, int64_t tiles, int slots, int halo = 2);
 
+// x schedule of the register-ring kernel (TBRArgs): segments of `seg`
+// planes; n1 pieces in whole rounds, then r leftover pieces cut at `split`
+// into A parts and nb2 (0 or r) B parts.
+struct XPlan {
+  int seg = 1, n1 = 0, r = 0, split = 0, nb2 = 0;
+};
+// Chosen by simulating greedy in-order dispatch onto `slots` resident
+// workgroups (cost of a piece: its planes + `fill` pipeline planes, rounded up
+// to chunks of U); cached per shape.  equal_only: no split (previous policy).
+XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_only = false);
+XPlan fixed_xplan(int64_t nx, int64_t tiles, int seg);
+
 }  // namespace hip
 }  // namespace heat3d

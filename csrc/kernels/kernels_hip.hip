@@ -31,6 +31,11 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <vector>
+#include <tuple>
+#include <mutex>
+#include <map>
+#include <functional>
 
 #include "hip_helpers.hpp"
 
@@ -436,6 +441,116 @@ int choose_segment(int64_t nx, int64_t tiles, int slots, int halo) {
     }
   }
   return std::max(1, pick);
+}
+
+XPlan fixed_xplan(int64_t nx, int64_t tiles, int seg) {
+  XPlan p;
+  p.seg = (int)std::max<int64_t>(1, std::min<int64_t>(seg, std::max<int64_t>(1, nx)));
+  const int64_t nxs = (nx + p.seg - 1) / p.seg;
+  p.n1 = (int)(tiles * nxs);
+  p.split = p.seg;
+  return p;
+}
+
+// Greedy list scheduling of the pieces, in dispatch order, on `slots`
+// workers; returns the makespan in plane-steps.
+static double simulate_xplan(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fill, int U,
+                             std::vector<double>& heap) {
+  const int64_t nxs = (nx + p.seg - 1) / p.seg;
+  auto cost = [&](int64_t len) {
+    const int64_t steps = len + fill;
+    return (double)((steps + U - 1) / U * U) + 2.0;  // + workgroup start-up
+  };
+  heap.assign((std::size_t)slots, 0.0);  // min-heap of worker free times
+  auto run = [&](double c) {
+    std::pop_heap(heap.begin(), heap.end(), std::greater<double>());
+    heap.back() += c;
+    std::push_heap(heap.begin(), heap.end(), std::greater<double>());
+  };
+  auto seg_len = [&](int64_t piece) {
+    const int64_t xs = piece / tiles;  // segment index slowest
+    const int64_t a = xs * p.seg;
+    return std::min<int64_t>(p.seg, nx - a);
+  };
+  for (int64_t i = 0; i < p.n1; ++i) run(cost(seg_len(i)));
+  for (int64_t i = 0; i < p.r; ++i) {
+    const int64_t len = seg_len(p.n1 + i);
+    run(cost(p.nb2 > 0 ? std::min<int64_t>(len, p.split) : len));
+  }
+  for (int64_t i = 0; i < p.nb2; ++i) {
+    const int64_t len = seg_len(p.n1 + i);
+    run(cost(std::max<int64_t>(0, len - p.split)));
+  }
+  double m = 0;
+  for (double t : heap) m = std::max(m, t);
+  (void)nxs;
+  return m;
+}
+
+XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_only) {
+  struct Key {
+    int64_t nx, tiles;
+    int slots, fill, U;
+    bool eq;
+    bool operator<(const Key& o) const {
+      return std::tie(nx, tiles, slots, fill, U, eq) < std::tie(o.nx, o.tiles, o.slots, o.fill, o.U, o.eq);
+    }
+  };
+  static std::mutex mu;
+  static std::map<Key, XPlan> cache;
+  const Key key{nx, tiles, slots, fill, U, equal_only};
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  XPlan best = fixed_xplan(nx, tiles, (int)std::max<int64_t>(1, nx));
+  double best_t = 1e300;
+  std::vector<double> heap;
+  const int64_t maxparts = std::min<int64_t>(nx, 64);
+  for (int64_t parts = 1; parts <= maxparts; ++parts) {
+    int64_t seg = (nx + parts - 1) / parts;
+    // segment steps in whole chunks of U
+    seg += (U - (seg + fill) % U) % U;
+    seg = std::min<int64_t>(seg, nx);
+    const int64_t nxs = (nx + seg - 1) / seg;
+    if (parts > 1 && nxs != parts) continue;  // duplicate of a smaller part count
+    const int64_t P = tiles * nxs;
+    if (P >= (1LL << 30)) break;
+    XPlan c;
+    c.seg = (int)seg;
+    const int64_t k = P / slots;
+    std::vector<int> splits{(int)seg};
+    if (!equal_only && k > 0 && P % slots != 0) {
+      c.n1 = (int)(k * slots);
+      c.r = (int)(P - c.n1);
+      for (int f = 1; f < 8; ++f) splits.push_back((int)std::max<int64_t>(1, seg * f / 8));
+      splits.push_back((int)((2 * seg + fill) / 3));
+      const int64_t left = (int64_t)c.r * seg;
+      splits.push_back((int)std::max<int64_t>(1, std::min<int64_t>(seg - 1, (left + slots - 1) / slots)));
+    } else {
+      c.n1 = (int)P;
+      c.r = 0;
+    }
+    for (int sp : splits) {
+      XPlan t = c;
+      if (t.r > 0) {
+        t.split = std::max(1, std::min(sp, (int)seg));
+        t.nb2 = t.split < seg ? t.r : 0;
+      } else {
+        t.split = (int)seg;
+        t.nb2 = 0;
+      }
+      const double m = simulate_xplan(t, nx, tiles, slots, fill, U, heap);
+      if (m < best_t - 1e-9) {
+        best_t = m;
+        best = t;
+      }
+    }
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = best;
+  return best;
 }
 
 template <typename Real, int V, int R, int WZ, int WY>

@@ -49,8 +49,16 @@ struct TBRArgs {
   int ylo_live, yhi_live;  // y rows present in memory
   int kb0, yb0;            // first column / row of tile (0, 0)
   int zstep, zring;        // tile stride along z, stored column ring
-  int nzb, nyb, seg;
-  int xq, xr;              // XCD remap: blocks per XCD (quotient / remainder)
+  int nzb, nyb;
+  // x schedule (XPlan, kernels_hip.hip): pieces = (tile, x segment of seg
+  // planes), segment index slowest.  The first n1 pieces fill whole rounds of
+  // resident workgroups; each of the r remaining pieces is cut at `split`
+  // into an A part and, if the B flag is set, a B part, dispatched after them,
+  // so the last round is filled longest-first instead of leaving CUs idle.
+  // Packed (seg | split << 16, r | B << 30): this struct must not grow — at
+  // 144 bytes the default fp64 variant starts spilling VGPRs.
+  int segsplit;
+  int n1, rb;
 };
 
 namespace {
@@ -105,13 +113,36 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   __shared__ unsigned long long s_red[WY][K];  // per-wave residual maxima
   if (flag_set(done)) return;
 
+  // Blocks are dispatched in index order, round-robin over the 8 XCDs; within
+  // each class the index is permuted so that consecutive pieces (neighbouring
+  // tiles) land on one XCD and share its L2.
+  auto remap = [](int i, int n) {
+    const int c = i & 7;
+    return c * (n >> 3) + min(c, n & 7) + (i >> 3);
+  };
   const int blk = blockIdx.x;
-  const int xcd = blk & 7;
-  int t = xcd * g.xq + min(xcd, g.xr) + (blk >> 3);
-  const int zb = t % g.nzb;
-  t /= g.nzb;
-  const int ybk = t % g.nyb;
-  const int xs = t / g.nyb;
+  int pc, part;
+  if (blk < g.n1) {
+    pc = remap(blk, g.n1);
+    part = 0;
+  } else if (blk < g.n1 + (g.rb & 0x3fffffff)) {
+    const int r = g.rb & 0x3fffffff;
+    pc = g.n1 + remap(blk - g.n1, r);
+    part = 1;
+  } else {
+    const int r = g.rb & 0x3fffffff;
+    pc = g.n1 + remap(blk - g.n1 - r, r);
+    part = 2;
+  }
+  const int zb = pc % g.nzb;
+  const int tq = pc / g.nzb;
+  const int ybk = tq % g.nyb;
+  const int xs = tq / g.nyb;
+  const int nxb = g.bhi[0] - g.blo[0];
+  const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
+  int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
+  if (part == 1 && (g.rb >> 30)) xhi_p = min(xhi_p, xlo_p + split);
+  if (part == 2) xlo_p = min(xlo_p + split, xhi_p);
 
   // the wave index is uniform: keep it (and every row / plane offset derived
   // from it) in SGPRs, so that a load is an SGPR base + one shared VGPR lane
@@ -123,8 +154,8 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
   const int k = tkb + lane * V;
   const int yb = tyb + wave * R;
   const int uylo = g.uylo, uyhi = g.uyhi;
-  const int xa = g.blo[0] + xs * g.seg;
-  const int xe = min(xa + g.seg, g.bhi[0]);
+  const int xa = g.blo[0] + xlo_p;
+  const int xe = g.blo[0] + xhi_p;
   const int64_t sx = g.sx, sy = g.sy;
 
   // per-lane column masks: in the box, stored.  The residual's column
@@ -402,26 +433,27 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.nzb = (int)std::max<int64_t>(1, (zspan + g.zstep - 1) / g.zstep);
   const int ystep = TYB - 2 * (K - 1);
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + ystep - 1) / ystep);
-  int seg = ks.L;
-  if (seg <= 0) {
-    static int slots = 0;
-    if (!slots)
-      slots = device_slots(reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q, NTS>), 64 * WY);
-    seg = choose_segment(b.extent(0), (int64_t)g.nzb * g.nyb, slots, 2 * K);
-    // a segment runs seg + 2(K-1) steps in chunks of U = lcm(Q, 3)
-    constexpr int U = Q == 3 ? 3 : 12;
-    const int steps = seg + 2 * (K - 1);
-    seg += (U - steps % U) % U;
+  static int slots = 0;
+  if (!slots)
+    slots = device_slots(reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q, NTS>), 64 * WY);
+  const int64_t ntiles = (int64_t)g.nzb * g.nyb;
+  const int64_t nxb = b.extent(0);
+  constexpr int U = Q == 3 ? 3 : 12;  // a piece runs its steps in chunks of U = lcm(Q, 3)
+  XPlan xp;
+  if (ks.L > 0) {
+    xp = fixed_xplan(nxb, ntiles, ks.L);  // explicit segment length, no split
+  } else {
+    xp = plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
   }
-  g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));
-  const int64_t nxs = (b.extent(0) + g.seg - 1) / g.seg;
-  const int64_t nblocks = (int64_t)g.nzb * g.nyb * nxs;
-  HEAT3D_CHECK(nblocks < (1LL << 31), "too many blocks");
-  g.xq = (int)(nblocks / 8);
-  g.xr = (int)(nblocks % 8);
+  HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tbr: x plan out of range");
+  g.segsplit = xp.seg | (xp.split << 16);
+  g.n1 = xp.n1;
+  g.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
+  const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
+  HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tbr: bad block count " << nblocks);
   if (std::getenv("HEAT3D_TRACE"))
-    std::fprintf(stderr, "[heat3d trace] tbr K=%d box x %lld: seg=%d tiles=%dx%d blocks=%lld\n", K,
-                 (long long)b.extent(0), g.seg, g.nzb, g.nyb, (long long)nblocks);
+    std::fprintf(stderr, "[heat3d trace] tbr K=%d box x %lld: seg=%d tiles=%dx%d blocks=%lld (n1=%d r=%d split=%d nb2=%d)\n",
+                 K, (long long)nxb, xp.seg, g.nzb, g.nyb, (long long)nblocks, xp.n1, xp.r, xp.split, xp.nb2);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tbr: residual slots " << p.slot << "+" << K);
   // Variants whose registers spill are slow and, with the ring fully unrolled,
   // have been miscompiled on ROCm 7.2 (tr4:1:4:1:16:0:4 produced wrong row-0
