@@ -459,7 +459,8 @@ static double simulate_xplan(const XPlan& p, int64_t nx, int64_t tiles, int slot
   const int64_t nxs = (nx + p.seg - 1) / p.seg;
   auto cost = [&](int64_t len) {
     const int64_t steps = len + fill;
-    return (double)((steps + U - 1) / U * U) + 2.0;  // + workgroup start-up
+    // + workgroup start-up and pipeline ramp
+    return (double)((steps + U - 1) / U * U) + 8.0;
   };
   heap.assign((std::size_t)slots, 0.0);  // min-heap of worker free times
   auto run = [&](double c) {
@@ -504,48 +505,37 @@ XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_o
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
   }
-  XPlan best = fixed_xplan(nx, tiles, (int)std::max<int64_t>(1, nx));
-  double best_t = 1e300;
+  // 1) equal segments from the round-count model (choose_segment), the
+  // policy the kernel sweeps were tuned with (profiles/kernel_sweep.md)
+  int seg0 = choose_segment(nx, tiles, slots, fill + 2);
+  seg0 += (U - (seg0 + fill) % U) % U;  // segment steps in whole chunks of U
+  XPlan best = fixed_xplan(nx, tiles, seg0);
+  if (equal_only || !(tiles > slots && tiles <= 2 * (int64_t)slots && tiles % slots != 0)) {
+    std::lock_guard<std::mutex> lk(mu);
+    cache[key] = best;
+    return best;
+  }
+  // 2) thin x boxes (an x slab of a 1024^2 face: 432 tiles on 256 CUs): one
+  // whole-x piece per tile, the first `slots` of them a full round, the rest
+  // cut in two and dispatched longest first so that the second round is
+  // filled.  Taken only if the greedy-dispatch model predicts >= 10% — on
+  // MI355X splitting long multi-round schedules (1024^3 fp64, 2049^3 fp32)
+  // lost 5-15% to equal segments although the model favoured it slightly
+  // (tools/probe_xplan.sh); the 128-plane slab gains 8%.
   std::vector<double> heap;
-  const int64_t maxparts = std::min<int64_t>(nx, 64);
-  for (int64_t parts = 1; parts <= maxparts; ++parts) {
-    int64_t seg = (nx + parts - 1) / parts;
-    // segment steps in whole chunks of U
-    seg += (U - (seg + fill) % U) % U;
-    seg = std::min<int64_t>(seg, nx);
-    const int64_t nxs = (nx + seg - 1) / seg;
-    if (parts > 1 && nxs != parts) continue;  // duplicate of a smaller part count
-    const int64_t P = tiles * nxs;
-    if (P >= (1LL << 30)) break;
-    XPlan c;
-    c.seg = (int)seg;
-    const int64_t k = P / slots;
-    std::vector<int> splits{(int)seg};
-    if (!equal_only && k > 0 && P % slots != 0) {
-      c.n1 = (int)(k * slots);
-      c.r = (int)(P - c.n1);
-      for (int f = 1; f < 8; ++f) splits.push_back((int)std::max<int64_t>(1, seg * f / 8));
-      splits.push_back((int)((2 * seg + fill) / 3));
-      const int64_t left = (int64_t)c.r * seg;
-      splits.push_back((int)std::max<int64_t>(1, std::min<int64_t>(seg - 1, (left + slots - 1) / slots)));
-    } else {
-      c.n1 = (int)P;
-      c.r = 0;
-    }
-    for (int sp : splits) {
-      XPlan t = c;
-      if (t.r > 0) {
-        t.split = std::max(1, std::min(sp, (int)seg));
-        t.nb2 = t.split < seg ? t.r : 0;
-      } else {
-        t.split = (int)seg;
-        t.nb2 = 0;
-      }
-      const double m = simulate_xplan(t, nx, tiles, slots, fill, U, heap);
-      if (m < best_t - 1e-9) {
-        best_t = m;
-        best = t;
-      }
+  const double base = simulate_xplan(best, nx, tiles, slots, fill, U, heap);
+  XPlan c = fixed_xplan(nx, tiles, (int)nx);
+  c.n1 = slots;
+  c.r = (int)(tiles - slots);
+  double best_t = base;
+  for (int f = 1; f < 8; ++f) {
+    XPlan t = c;
+    t.split = std::max(1, c.seg * f / 8);
+    t.nb2 = t.r;
+    const double m = simulate_xplan(t, nx, tiles, slots, fill, U, heap);
+    if (m < best_t - 1e-9 && m < 0.9 * base) {
+      best_t = m;
+      best = t;
     }
   }
   std::lock_guard<std::mutex> lk(mu);
