@@ -20,12 +20,18 @@ void set_threads(int n) {
   if (n > 0) omp_set_num_threads(n);
 }
 
+// Boxes below this many points run on the calling thread: the boundary pieces
+// and deep-halo slabs of small decomposed grids are a few hundred points, and a
+// parallel region per piece costs more than the piece (badly so when the host
+// is oversubscribed, e.g. several ranks or test workers per core).
+static inline bool omp_worth(int64_t points) { return points >= (int64_t(1) << 15); }
+
 template <typename Real>
 static void init_t(const InitParams& p) {
   Real* f = static_cast<Real*>(p.field);
   const Layout& L = p.L;
   // every ghost plane (deep x halos included) gets its Dirichlet ghost rows
-#pragma omp parallel for collapse(2) schedule(static)
+#pragma omp parallel for collapse(2) schedule(static) if (omp_worth(static_cast<int64_t>(L.elems)))
   for (int64_t i = -L.gx; i < L.n[0] + L.gx; ++i)
     for (int64_t j = -L.gy; j < L.n[1] + L.gy; ++j) {
       const int64_t gi = p.gstart[0] + i, gj = p.gstart[1] + j;
@@ -69,7 +75,7 @@ static void stencil_t(const StencilParams& p) {
     else return cpu_row_kernels().f32;
   }();
   const int64_t nk = b.extent(2);
-#pragma omp parallel for collapse(2) schedule(static) reduction(max : resbits)
+#pragma omp parallel for collapse(2) schedule(static) reduction(max : resbits) if (omp_worth(b.volume()))
   for (int64_t i = b.lo[0]; i < b.hi[0]; ++i)
     for (int64_t j = b.lo[1]; j < b.hi[1]; ++j) {
       const int64_t c = L.index(i, j, b.lo[2]);
@@ -117,7 +123,7 @@ void stencil(DType t, const StencilParams& p) {
 template <typename Real>
 static void pack_t(const Real* f, const Layout& L, const Box& b, Real* buf) {
   const int64_t ey = b.extent(1), ez = b.extent(2);
-#pragma omp parallel for collapse(2) schedule(static)
+#pragma omp parallel for collapse(2) schedule(static) if (omp_worth(b.volume()))
   for (int64_t i = b.lo[0]; i < b.hi[0]; ++i)
     for (int64_t j = b.lo[1]; j < b.hi[1]; ++j) {
       const int64_t o = ((i - b.lo[0]) * ey + (j - b.lo[1])) * ez;
@@ -128,7 +134,7 @@ static void pack_t(const Real* f, const Layout& L, const Box& b, Real* buf) {
 template <typename Real>
 static void unpack_t(Real* f, const Layout& L, const Box& b, const Real* buf) {
   const int64_t ey = b.extent(1), ez = b.extent(2);
-#pragma omp parallel for collapse(2) schedule(static)
+#pragma omp parallel for collapse(2) schedule(static) if (omp_worth(b.volume()))
   for (int64_t i = b.lo[0]; i < b.hi[0]; ++i)
     for (int64_t j = b.lo[1]; j < b.hi[1]; ++j) {
       const int64_t o = ((i - b.lo[0]) * ey + (j - b.lo[1])) * ez;
@@ -152,7 +158,7 @@ template <typename Real>
 static void copy_t(const Real* src, const Layout& Ls, const Box& bs, Real* dst, const Layout& Ld,
                    const Box& bd) {
   const int64_t ex = bs.extent(0), ey = bs.extent(1), ez = bs.extent(2);
-#pragma omp parallel for collapse(2) schedule(static)
+#pragma omp parallel for collapse(2) schedule(static) if (omp_worth(bs.volume()))
   for (int64_t i = 0; i < ex; ++i)
     for (int64_t j = 0; j < ey; ++j)
       std::memcpy(dst + Ld.index(bd.lo[0] + i, bd.lo[1] + j, bd.lo[2]),
