@@ -72,6 +72,10 @@ std::unique_ptr<Comm> make_socket_comm(int rank, int size, net::Bootstrap& boot)
 std::unique_ptr<Comm> make_socket_comm_from_table(int rank, int size, int listen_fd,
                                                   const std::vector<std::string>& addrs);
 
+// A host transport (socket) used by a GPU backend: device buffers are staged
+// through host memory on the caller's stream (the reference's MPI data path).
+std::unique_ptr<Comm> make_staged_comm(std::unique_ptr<Comm> inner);
+
 // RCCL: `unique_id` is the 128-byte ncclUniqueId from rank 0.
 bool rccl_available();
 std::string rccl_unique_id();

@@ -1348,6 +1348,7 @@ std::unique_ptr<Solver> make_solver(const Config& cfg, const RankPlacement& w) {
     case CommKind::Socket: {
       net::Bootstrap boot(rank, size, master, bport);
       comm = make_socket_comm(rank, size, boot);
+      if (bk == BackendKind::Hip) comm = make_staged_comm(std::move(comm));
       nranks = size;
       break;
     }

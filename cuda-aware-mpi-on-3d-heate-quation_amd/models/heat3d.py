@@ -122,7 +122,7 @@ class HeatSolver:
                 comm = "rccl" if use_gpu else "socket"
             else:
                 comm = "local"
-        if comm in ("rccl", "socket"):
+        if comm in ("rccl", "socket", "staged"):
             cargs = native_comm_args(comm, group=group)
         else:
             from ..parallel.distributed import NativeCommArgs

@@ -10,7 +10,10 @@ communicators:
   ncclSend/ncclRecv on device pointers over xGMI; the residual is an
   ncclAllReduce(max) on the device (replaces heat3D.cu:610-755, 1037-1063).
 * ``socket`` — CPU backend: each rank opens a listening TCP socket, the
-  address table is all-gathered, the native SocketComm builds a mesh.
+  address table is all-gathered, the native SocketComm builds a mesh.  With
+  the HIP backend the same transport is wrapped in StagedComm (device buffers
+  staged through host memory, as the reference's MPI path does); ``staged``
+  forces that wrapper on the CPU backend as well.
 """
 from __future__ import annotations
 
@@ -106,12 +109,12 @@ def native_comm_args(kind: str, group=None) -> NativeCommArgs:
         obj = [native().rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=group)
         return NativeCommArgs(rank, size, "rccl", unique_id=obj[0])
-    if kind == "socket":
+    if kind in ("socket", "staged"):
         fd, port = native().socket_listen()
         me = f"{_route_ip(os.environ.get('MASTER_ADDR', '127.0.0.1'))}:{port}"
         table: List[Optional[str]] = [None] * size
         dist.all_gather_object(table, me, group=group)
-        return NativeCommArgs(rank, size, "socket", listen_fd=fd, addrs=[str(a) for a in table])
+        return NativeCommArgs(rank, size, kind, listen_fd=fd, addrs=[str(a) for a in table])
     raise ValueError(f"unknown native comm kind {kind!r}")
 
 

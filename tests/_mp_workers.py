@@ -68,3 +68,47 @@ def torch_reference_worker(rank, world, port, outdir, n, eps, decomp):
             f.write(f"{r['conv_iter']} {100.0 * t[0].item() / t[1].item()!r}\n")
     dist.barrier()
     dist.destroy_process_group()
+
+
+def native_staged_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, extra_args=()):
+    """Native engine, HIP backend on the one visible GPU, socket transport with
+    host staging (RCCL refuses several ranks on one device): the multi-process
+    GPU schedule — overlapped streams, deep halos, lagged all-reduce — across
+    real processes."""
+    dist = _init(rank, world, port)
+    import heat3d_amd
+
+    s = heat3d_amd.HeatSolver((n, n, n), 10 ** 6, eps, backend="hip", comm="socket", decomp=decomp,
+                              dtype=dtype, device=0, extra_args=list(extra_args))
+    assert s.native.comm_name == "staged-socket", s.native.comm_name
+    r = s.run()
+    assert s.native.verify_halos() == 0
+    g = s.gather()
+    if rank == 0:
+        np.save(os.path.join(outdir, "field.npy"), g)
+        with open(os.path.join(outdir, "result.txt"), "w") as f:
+            f.write(f"{r['conv_iter']} {r['error_percent']!r}\n")
+    else:
+        assert g is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def native_staged_cpu_worker(rank, world, port, outdir, n, eps, decomp, extra_args=()):
+    """CPU backend through the staging wrapper (comm="staged"): same schedule
+    and transport as the GPU staged path, copies are host memcpy."""
+    dist = _init(rank, world, port)
+    import heat3d_amd
+
+    s = heat3d_amd.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", comm="staged", decomp=decomp,
+                              threads=2, extra_args=list(extra_args))
+    assert s.native.comm_name == "staged-socket", s.native.comm_name
+    r = s.run()
+    assert s.native.verify_halos() == 0
+    g = s.gather()
+    if rank == 0:
+        np.save(os.path.join(outdir, "field.npy"), g)
+        with open(os.path.join(outdir, "result.txt"), "w") as f:
+            f.write(f"{r['conv_iter']}\n")
+    dist.barrier()
+    dist.destroy_process_group()

@@ -91,3 +91,17 @@ def test_native_socket_temporal_blocks(h3d, tmp_path, world, decomp):
     r1 = single.run()
     assert int(open(tmp_path / "result.txt").read().split()[0]) == r1["conv_iter"]
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
+
+
+@pytest.mark.parametrize("world,decomp,temporal", [(2, (2, 1, 1), "3"), (4, (2, 2, 1), "3"), (2, (1, 2, 1), "1")])
+def test_staged_comm_cpu(h3d, tmp_path, world, decomp, temporal):
+    """StagedComm (the GPU ranks' host-staged socket transport) driven on the
+    CPU backend: bitwise equal to the single-process solve."""
+    from _mp_workers import native_staged_cpu_worker
+
+    n, eps = 23, 1e-4
+    _spawn(native_staged_cpu_worker, world, str(tmp_path), n, eps, decomp, ["--temporal", temporal])
+    single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", extra_args=["--temporal", "1"])
+    r1 = single.run()
+    assert int(open(tmp_path / "result.txt").read().split()[0]) == r1["conv_iter"]
+    assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
