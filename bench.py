@@ -49,6 +49,9 @@ def main() -> int:
     ap.add_argument("--kernel2", default="auto", help="temporally blocked sweep kernel (tbK / trK[:V:R:WZ:WY:L:Q])")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: split the grid into this many subdomains on one GPU (not the headline)")
+    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "socket"],
+                    help="multi-process transport: auto = RCCL over xGMI; socket = host-staged TCP "
+                         "(rehearses the N>1 launch with several ranks on one GPU, which RCCL refuses)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -67,7 +70,7 @@ def main() -> int:
               f"python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}",
               file=sys.stderr)
         return 2
-    info, group = init_process_group("nccl" if world > 1 else None)
+    info, group = init_process_group(("gloo" if args.comm == "socket" else "nccl") if world > 1 else None)
     rank = info.rank
     if ext.device_count() < 1:
         print("bench.py: no HIP device visible", file=sys.stderr)
@@ -93,7 +96,7 @@ def main() -> int:
         return HeatSolver(N, iter_max=iter_max, eps=eps, dtype=args.dtype, backend="hip",
                           decomp=dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
-                          device=dev, group=group, virtual_ranks=args.virtual_ranks,
+                          device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
                           extra_args=["--temporal", str(args.temporal), "--kernel2", args.kernel2])
 
     s = make(0.0, 1 << 40)
@@ -116,6 +119,7 @@ def main() -> int:
     value = points * args.steps / dt / 1e9
     esize = 8 if args.dtype == "fp64" else 4
     kernel = s.kernel
+    comm_name = s.native.comm_name
     del s
 
     ttc = None
@@ -147,7 +151,8 @@ def main() -> int:
                    "grid": list(N),
                    "global_batch": 1, "seq_len": G, "parallelism": f"{'slab' if dims[1] == dims[2] == 1 and dims[0] > 1 else 'block'} {par}"
                    + (f" ({args.virtual_ranks} virtual ranks on 1 GPU)" if args.virtual_ranks > 1 else ""),
-                   "kernel": kernel, "graph": not args.no_graph, "overlap": not args.no_overlap},
+                   "kernel": kernel, "graph": not args.no_graph, "overlap": not args.no_overlap,
+                   "comm": comm_name},
         "glups_per_gpu": round(value / world, 3),
         "effective_hbm_tbps_per_gpu": round(value / world * 2 * esize / 1e3, 3),
         "vs_roofline": round(value / roofline_glups(esize, world), 4),
