@@ -27,3 +27,26 @@ def test_staged_multiprocess_gpu_bitwise(h3d, gpu, tmp_path, world, decomp, temp
     it, err = open(tmp_path / "result.txt").read().split()
     assert int(it) == r1["conv_iter"]
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
+
+
+def test_cli_two_processes_one_gpu(heat3d_bin, gpu, tmp_path):
+    """The heat3d CLI launched torchrun-style (RANK / WORLD_SIZE env) as two
+    processes on the one GPU with --comm socket: HIP kernels, host-staged
+    halos, the reference's golden iteration count (27^3, eps 1e-4)."""
+    import os
+    import subprocess
+
+    port = free_port()
+    procs = []
+    for r in range(2):
+        e = dict(os.environ)
+        e.update({"WORLD_SIZE": "2", "RANK": str(r), "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": str(port), "HEAT3D_BOOTSTRAP_PORT": str(port)})
+        procs.append(subprocess.Popen([heat3d_bin, "27", "27", "27", "100000", "1e-4", "--backend", "hip",
+                                       "--comm", "socket", "--temporal", "3"], cwd=tmp_path, env=e,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "converged in 1725 iterations" in outs[0][0]
+    assert "comm=staged-socket ranks=2" in outs[0][0], outs[0][0]
+    assert (tmp_path / "output" / "out.dat").read_text().count("ZONE") == 2
