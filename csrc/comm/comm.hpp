@@ -76,6 +76,10 @@ std::unique_ptr<Comm> make_socket_comm_from_table(int rank, int size, int listen
 // through host memory on the caller's stream (the reference's MPI data path).
 std::unique_ptr<Comm> make_staged_comm(std::unique_ptr<Comm> inner);
 
+// Performance proxy: rank `rank` of a `size`-rank job alone on one device,
+// peers emulated (phantom_comm.cpp).
+std::unique_ptr<Comm> make_phantom_comm(int rank, int size);
+
 // RCCL: `unique_id` is the 128-byte ncclUniqueId from rank 0.
 bool rccl_available();
 std::string rccl_unique_id();

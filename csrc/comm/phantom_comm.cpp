@@ -1,0 +1,72 @@
+// heat3d-mi355x — PhantomComm: one rank of a P-rank job, alone on one device.
+//
+// A performance proxy, not a transport: the process builds rank r's subdomain
+// of a P-way decomposition and runs that rank's exact schedule (interior and
+// boundary kernels, deep halos, streams, lagged all-reduce), while the peers
+// are phantoms.  Received halos are filled with a same-sized face this rank
+// sends (numerically meaningless, finite), every exchange occupies the stream
+// for bytes-per-peer / HEAT3D_PHANTOM_GBPS (a one-workgroup delay kernel — an
+// RCCL p2p kernel also holds a CU while it moves data), and every all-reduce
+// for HEAT3D_PHANTOM_ALLREDUCE_US.  This is how the per-GPU time of the
+// multi-GPU bench is measured on the one-GPU box (tools/rank_proxy.py).
+#include <cstdlib>
+#include <map>
+
+#include "comm.hpp"
+
+namespace heat3d {
+
+namespace {
+
+double env_or(const char* name, double dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atof(e) : dflt;
+}
+
+class PhantomComm final : public Comm {
+ public:
+  PhantomComm(int rank, int size)
+      : rank_(rank), size_(size), gbps_(env_or("HEAT3D_PHANTOM_GBPS", 50.0)),
+        ar_us_(env_or("HEAT3D_PHANTOM_ALLREDUCE_US", 20.0)) {
+    HEAT3D_CHECK(rank >= 0 && rank < size, "phantom rank " << rank << " of " << size);
+  }
+  const char* name() const override { return "phantom"; }
+  int size() const override { return size_; }
+  std::vector<int> local_ranks() const override { return {rank_}; }
+  bool device_buffers() const override { return true; }
+  bool capturable() const override { return true; }
+
+  void exchange(const std::vector<Transfer>& xs, Backend& be, StreamId s) override {
+    std::map<int, std::size_t> per_peer;
+    for (const auto& x : xs)
+      if (x.dst_rank == rank_ && x.src_rank != rank_) per_peer[x.src_rank] += x.bytes;
+    std::size_t worst = 0;
+    for (const auto& kv : per_peer) worst = std::max(worst, kv.second);
+    if (worst && gbps_ > 0) be.delay(worst / (gbps_ * 1e3), s);  // bytes / (GB/s) in us
+    for (const auto& x : xs) {
+      if (x.dst_rank != rank_ || x.src_rank == rank_) continue;
+      const void* src = nullptr;
+      for (const auto& y : xs)
+        if (y.src_rank == rank_ && y.bytes == x.bytes) src = y.src;
+      if (src) be.copy(x.dst, src, x.bytes, CopyKind::D2D, s);
+    }
+  }
+  void allreduce(void*, std::size_t, RedType, RedOp, Backend& be, StreamId s) override {
+    if (ar_us_ > 0) be.delay(ar_us_, s);
+  }
+  void send(const void*, std::size_t, int, Backend&, StreamId) override {}
+  void recv(void*, std::size_t, int, Backend&, StreamId) override {}
+  void barrier(Backend&) override {}
+
+ private:
+  int rank_, size_;
+  double gbps_, ar_us_;
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_phantom_comm(int rank, int size) {
+  return std::unique_ptr<Comm>(new PhantomComm(rank, size));
+}
+
+}  // namespace heat3d

@@ -105,6 +105,9 @@ std::unique_ptr<Solver> create_solver(const std::vector<std::string>& args, int 
     HEAT3D_CHECK(bk == BackendKind::Hip, "rccl comm needs the HIP backend");
     comm = make_rccl_comm(rank, size, std::string(unique_id), dev);
     nranks = size;
+  } else if (comm_kind == "phantom") {
+    comm = make_phantom_comm(rank, size);
+    nranks = size;
   } else if (comm_kind == "socket" || comm_kind == "staged") {
     // a GPU backend always stages through host memory; "staged" forces the
     // wrapper on the CPU backend too (tests of the staging logic without a GPU)

@@ -92,7 +92,8 @@ class HeatSolver:
                  decomp: Optional[Sequence[int]] = None, virtual_ranks: int = 1,
                  kernel: str = "auto", graph: bool = True, overlap: bool = True,
                  check_every: int = 64, graph_chunk: int = 32, device: Optional[int] = None,
-                 threads: int = 0, extra_args: Sequence[str] = (), group=None):
+                 threads: int = 0, extra_args: Sequence[str] = (), group=None,
+                 phantom: Optional[Sequence[int]] = None):
         ext = native()
         self.model = HeatEquation3D(tuple(int(v) for v in n))  # type: ignore[arg-type]
         args: List[str] = [str(int(v)) for v in n] + [str(int(iter_max)), _fmt(eps)]
@@ -122,7 +123,13 @@ class HeatSolver:
                 comm = "rccl" if use_gpu else "socket"
             else:
                 comm = "local"
-        if comm in ("rccl", "socket", "staged"):
+        if phantom is not None:
+            # performance proxy: rank phantom[0] of a phantom[1]-rank job, peers emulated
+            from ..parallel.distributed import NativeCommArgs
+
+            comm = "phantom"
+            cargs = NativeCommArgs(int(phantom[0]), int(phantom[1]), "phantom")
+        elif comm in ("rccl", "socket", "staged"):
             cargs = native_comm_args(comm, group=group)
         else:
             from ..parallel.distributed import NativeCommArgs

@@ -156,3 +156,20 @@ def test_phase_timers(h3d):
     t = dict(s.native.phase_times())
     assert set(t) == {"interior_ms", "halo_ms", "shell_ms", "reduce_check_ms", "iteration_ms"}
     assert t["iteration_ms"] >= t["interior_ms"] >= 0
+
+
+@pytest.mark.parametrize("rank,size,decomp,temporal", [(1, 4, (4, 1, 1), "3"), (0, 2, (2, 1, 1), "1"),
+                                                       (3, 8, (2, 2, 2), "3")])
+def test_phantom_rank_proxy_runs(h3d, rank, size, decomp, temporal, monkeypatch):
+    """PhantomComm (tools/rank_proxy.py): one rank of a P-rank job alone in the
+    process builds only its subdomain and runs its whole schedule, every
+    issued iteration accounted for, nothing converges at eps 0."""
+    monkeypatch.setenv("HEAT3D_PHANTOM_ALLREDUCE_US", "0")
+    s = h3d.HeatSolver((20, 20, 20), 1 << 40, 0.0, backend="cpu", decomp=decomp, phantom=(rank, size),
+                       threads=2, extra_args=["--temporal", temporal])
+    assert s.native.comm_name == "phantom"
+    s.initialize()
+    s.step(13)
+    s.synchronize()
+    st = s.state()
+    assert st["iter"] == 13 and st["done"] == 0, st

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Per-GPU time of the multi-GPU bench, measured on one GPU (performance proxy).
+
+Runs rank R of a P-rank decomposition of the bench grid alone on the device
+(PhantomComm, csrc/comm/phantom_comm.cpp): that rank's own kernels, streams and
+schedule — interior sweep || (emulated halo exchange -> boundary slabs),
+lagged all-reduce — with the peers' traffic replaced by a D2D copy plus a
+one-workgroup delay of bytes / --gbps per exchange and --ar-us per all-reduce.
+The projected node GLUPS assumes every rank takes as long as this one.  It
+is a model input, not a measurement of xGMI; the driver's multi-GPU bench run
+is the real number.
+
+  python tools/rank_proxy.py --ranks 8 [--rank 1] [--grid 1024] [--gbps 50] [--ar-us 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=-1, help="default: an inner rank (two neighbours)")
+    ap.add_argument("--grid", type=int, default=1024)
+    ap.add_argument("--decomp", default="auto")
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--gbps", type=float, default=50.0, help="emulated halo bandwidth per peer (GB/s)")
+    ap.add_argument("--ar-us", type=float, default=20.0, help="emulated all-reduce latency (us)")
+    ap.add_argument("--backend", default="hip")
+    ap.add_argument("--extra", default="", help="extra solver flags, e.g. '--no-overlap'")
+    args = ap.parse_args()
+
+    os.environ["HEAT3D_PHANTOM_GBPS"] = str(args.gbps)
+    os.environ["HEAT3D_PHANTOM_ALLREDUCE_US"] = str(args.ar_us)
+    from heat3d_amd import HeatSolver
+    from heat3d_amd.parallel import best_dims_for
+
+    N = (args.grid,) * 3
+    P = args.ranks
+    if args.decomp in ("auto", "slab", "block"):
+        dims = best_dims_for(N, P, None if args.decomp == "auto" else args.decomp)
+    else:
+        dims = tuple(int(v) for v in args.decomp.lower().split("x"))
+    r = args.rank if args.rank >= 0 else min(1, P - 1)
+    s = HeatSolver(N, iter_max=1 << 40, eps=0.0, dtype=args.dtype, backend=args.backend, decomp=dims,
+                   device=0 if args.backend == "hip" else None, phantom=(r, P),
+                   extra_args=args.extra.split() if args.extra else ())
+    s.initialize()
+    s.step(args.warmup)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.step(args.steps)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    st = s.state()
+    assert st["iter"] == args.warmup + args.steps, st
+    out = {"proxy": "phantom rank", "rank": r, "ranks": P, "dims": list(dims), "grid": args.grid,
+           "dtype": args.dtype, "gbps": args.gbps, "ar_us": args.ar_us, "extra": args.extra,
+           "ms_per_step": round(dt / args.steps * 1e3, 4), "kernel": s.kernel,
+           "projected_node_glups": round(s.interior_points * args.steps / dt / 1e9, 2)}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
