@@ -43,6 +43,15 @@ def run_bench(args, gpus, timeout):
     return out
 
 
+def run_proxy(args, timeout):
+    """tools/rank_proxy.py: one inner rank of the 8-rank job alone on the GPU."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "rank_proxy.py")] + args
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    if p.returncode != 0:
+        raise RuntimeError(f"{' '.join(cmd)} failed ({p.returncode}):\n{p.stderr[-3000:]}")
+    return json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+
+
 def config1(steps):
     import heat3d_amd
     from heat3d_amd.utils import golden
@@ -82,7 +91,9 @@ def main():
                        "bench": run_bench(extra, 8, a.timeout)}
             else:
                 row = {"config": 3, "name": "1024^3 fp64 slab 8x1x1", "mode": "proxy: 8 virtual ranks on 1 GPU",
-                       "bench": run_bench(extra + ["--virtual-ranks", "8"], 1, a.timeout)}
+                       "bench": run_bench(extra + ["--virtual-ranks", "8"], 1, a.timeout),
+                       "phantom": run_proxy(["--ranks", "8", "--grid", "1024", "--decomp", "8x1x1",
+                                             "--gbps", "64", "--steps", str(4 * a.steps)], a.timeout)}
         elif c == 4:
             extra = ["--grid", "2048", "--dtype", "fp32", "--decomp", "2x2x2", "--steps", str(a.steps // 2),
                      "--warmup", "4", "--converge-eps", "0"]
@@ -91,7 +102,9 @@ def main():
                        "bench": run_bench(extra, 8, a.timeout)}
             else:
                 row = {"config": 4, "name": "2048^3 fp32 block 2x2x2", "mode": "proxy: 8 virtual ranks on 1 GPU",
-                       "bench": run_bench(extra + ["--virtual-ranks", "8"], 1, a.timeout)}
+                       "bench": run_bench(extra + ["--virtual-ranks", "8"], 1, a.timeout),
+                       "phantom": run_proxy(["--ranks", "8", "--grid", "2048", "--dtype", "fp32", "--decomp", "2x2x2",
+                                             "--gbps", "64", "--steps", str(2 * a.steps)], a.timeout)}
         elif c == 5:
             pts = []
             for g in ([1, 2, 4, 8] if real else [1]):
@@ -126,6 +139,13 @@ def markdown(rows):
             ttc = (f"{t['iterations']} it in {t['seconds']:.3f} s at eps {t['eps']:g}" if t else "—")
             out.append(f"| {r['config']} | {r['name']} | {r['mode']} | {b['dtype']} | {'x'.join(map(str, c['grid']))} | "
                        f"{c['parallelism']} | `{c['kernel']}` | {b['value']} | {b['ms_per_step']} | {ttc} |")
+        ph = r.get("phantom")
+        if ph:
+            g = ph["grid"]
+            out.append(f"| {r['config']} | {r['name']} | proxy: phantom rank {ph['rank']} of {ph['ranks']} alone on 1 GPU, "
+                       f"{ph['gbps']:g} GB/s emulated links (projected node GLUPS) | {ph['dtype']} | {g}^3 | "
+                       f"{'x'.join(map(str, ph['dims']))} | `{ph['kernel']}` | {ph['projected_node_glups']} | "
+                       f"{ph['ms_per_step']} | — |")
     return "\n".join(out) + "\n"
 
 
