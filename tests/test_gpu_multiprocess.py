@@ -50,3 +50,19 @@ def test_cli_two_processes_one_gpu(heat3d_bin, gpu, tmp_path):
     assert "converged in 1725 iterations" in outs[0][0]
     assert "comm=staged-socket ranks=2" in outs[0][0], outs[0][0]
     assert (tmp_path / "output" / "out.dat").read_text().count("ZONE") == 2
+
+
+@pytest.mark.parametrize("rank,size,decomp", [(1, 4, (4, 1, 1)), (5, 8, (2, 2, 2))])
+def test_phantom_rank_gpu(h3d, gpu, rank, size, decomp, monkeypatch):
+    """PhantomComm on the GPU (tools/rank_proxy.py): one rank's full overlapped
+    schedule with emulated halo delay kernels; every issued iteration checked."""
+    monkeypatch.setenv("HEAT3D_PHANTOM_GBPS", "50")
+    monkeypatch.setenv("HEAT3D_PHANTOM_ALLREDUCE_US", "5")
+    s = h3d.HeatSolver((97, 97, 97), 1 << 40, 0.0, backend="hip", device=0, decomp=decomp,
+                       phantom=(rank, size), extra_args=["--temporal", "3"])
+    assert s.native.comm_name == "phantom"
+    s.initialize()
+    s.step(40)
+    s.synchronize()
+    st = s.state()
+    assert st["iter"] == 40 and st["done"] == 0, st
