@@ -2,33 +2,51 @@
 """Headline benchmark: GLUPS of the FTCS 7-point heat solver, 1024^3 fp64.
 
 BASELINE.json metric "GLUPS (cell-updates/sec, whole node) + time-to-converge,
-1024^3 fp64 grid".  One process per GPU (torchrun); the global grid is fixed
-(strong scaling): 1 GPU -> 1x1x1, N GPUs -> N x 1 x 1 slabs (BASELINE config
-3: 1D slab decomposition + 2-neighbour halo over xGMI, RCCL on device
+1024^3 fp64 grid".  One process per GPU; the global grid is fixed (strong
+scaling): 1 GPU -> 1x1x1, N GPUs -> N x 1 x 1 slabs (BASELINE config 3: 1D
+slab decomposition + 2-neighbour halo over xGMI, RCCL send/recv on device
 pointers).  Every timed step is a full iteration of the production loop:
-interior sweep || (halo exchange -> boundary shell), fused residual, RCCL
+interior sweep || (halo exchange -> boundary slabs), fused residual, RCCL
 all-reduce(max) of the residual and the device-side convergence check
 (eps = 0 so it never stops early).  Synthetic data = the reference's analytic
-initial/boundary condition.
+initial/boundary condition (heat3D.cu:408-453).
+
+Launch (the reference: ``mpirun -n P ./heat3D ...``, heat3D.cu:203-205):
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
+      N > 1 without a launcher: this process starts N fresh worker processes
+      (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment) before
+      touching the GPU, waits for them under a watchdog and exits with the
+      worst return code; rank 0 prints the JSON line.
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+      one rank per process as launched (RANK / WORLD_SIZE from torchrun).
+
+torch.distributed (gloo) is used only to bootstrap: the ncclUniqueId
+broadcast, host barriers and the max-over-ranks of the timed interval.  All
+per-iteration traffic goes through the native RCCL communicator.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "GLUPS (cell-updates/sec, whole node) + time-to-converge, 1024^3 fp64 grid"
+BASELINE_METRIC = "GLUPS (cell-updates/sec, whole node) + time-to-converge, 1024^3 fp64 grid"
 
 
-def main() -> int:
+def metric_name(grid: str, dtype: str) -> str:
+    return f"GLUPS (cell-updates/sec, whole node) + time-to-converge, {grid} {dtype} grid"
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -51,31 +69,107 @@ def main() -> int:
                     help="diagnostic: split the grid into this many subdomains on one GPU (not the headline)")
     ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "socket"],
                     help="multi-process transport: auto = RCCL over xGMI; socket = host-staged TCP "
-                         "(rehearses the N>1 launch with several ranks on one GPU, which RCCL refuses)")
+                         "(rehearses the N>1 launch with several ranks on one GPU)")
+    ap.add_argument("--rccl-host-split", action="store_true",
+                    help="testing: give every rank its own NCCL_HOSTID so that RCCL accepts several "
+                         "ranks on one GPU (its traffic then takes RCCL's network transport over "
+                         "loopback); exercises the real RCCL send/recv/all-reduce path on a 1-GPU box")
+    ap.add_argument("--timeout", type=float, default=1500.0,
+                    help="watchdog (s): a launched job that runs longer is killed and exits non-zero")
     ap.add_argument("--json-out", default="")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+# ---------------------------------------------------------------------------
+# launcher: N fresh worker processes, started before anything touches the GPU
+
+def _free_port() -> int:
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args, argv) -> int:
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HEAT3D_BENCH_WORKER="1", HEAT3D_WATCHDOG_S=env.get("HEAT3D_WATCHDOG_S", "300"))
+        if args.rccl_host_split:
+            env.update(NCCL_HOSTID=f"heat3d-bench-rank{r}", NCCL_SOCKET_IFNAME="lo")
+        # each worker leads its own process group so that the watchdog can end
+        # it together with anything it started
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv),
+                                      env=env, start_new_session=True))
+    deadline = time.monotonic() + args.timeout
+    rc = 0
+    failed_at = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and failed_at is None:
+            failed_at = time.monotonic()
+            rc = bad[0]
+        if all(c is not None for c in codes):
+            break
+        now = time.monotonic()
+        # one rank failed: give its peers 20 s to notice (their native watchdogs
+        # abort the communicators), then end them
+        if now > deadline or (failed_at is not None and now - failed_at > 20):
+            if now > deadline:
+                print(f"bench.py: watchdog: job exceeded {args.timeout:.0f} s, killing workers",
+                      file=sys.stderr, flush=True)
+                rc = rc or 124
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(0.1)
+    for p in procs:
+        c = p.returncode
+        if c not in (0, None) and rc == 0:
+            rc = c
+    if rc < 0:
+        rc = 128 - rc
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# one rank
+
+def run_rank(args) -> int:
     import torch
 
     import heat3d_amd
     from heat3d_amd import HeatSolver
-    from heat3d_amd.parallel import best_dims_for, dims_create
-    from heat3d_amd.parallel.distributed import barrier, init_process_group, max_over_ranks
+    from heat3d_amd.parallel import best_dims_for
+    from heat3d_amd.parallel.distributed import all_gather_objects, barrier, init_process_group, max_over_ranks
     from heat3d_amd.utils.metrics import roofline_glups
 
     ext = heat3d_amd.native()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
-        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with "
-              f"python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}",
-              file=sys.stderr)
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
-    info, group = init_process_group(("gloo" if args.comm == "socket" else "nccl") if world > 1 else None)
+    # torch.distributed is the bootstrap only (gloo): the per-iteration halo and
+    # all-reduce traffic goes through the native RCCL communicator
+    info, group = init_process_group("gloo" if world > 1 else None)
     rank = info.rank
-    if ext.device_count() < 1:
+    ndev = ext.device_count()
+    if ndev < 1:
         print("bench.py: no HIP device visible", file=sys.stderr)
         return 2
-    dev = info.local_rank % ext.device_count()
+    dev = info.local_rank % ndev
     torch.cuda.set_device(dev)
 
     G = args.grid
@@ -101,8 +195,17 @@ def main() -> int:
 
     s = make(0.0, 1 << 40)
     s.initialize()
-    s.step(args.warmup)
+    s.step(max(1, args.warmup))
     s.synchronize()
+    # race detection before timing: every face sent by the warm-up exchange
+    # must match, bit for bit, the ghost layer the neighbour received
+    bad_faces = s.native.verify_halos()
+    if bad_faces:
+        print(f"bench.py: rank {rank}: {bad_faces} halo face(s) differ after warm-up", file=sys.stderr)
+        return 3
+    warm = s.native.iterations_issued
+    s.prepare_steps(args.steps)  # capture the graphs the timed steps replay (untimed)
+    g0 = s.native.graph_launches
     barrier(group)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -112,14 +215,20 @@ def main() -> int:
     barrier(group)
     t1 = time.perf_counter()
     dt = max_over_ranks(t1 - t0, group)
+    graph_launches = s.native.graph_launches - g0
     st = s.state()
     # every issued iteration must have been checked and none skipped
-    assert st["iter"] == args.warmup + args.steps and st["done"] == 0, st
+    assert st["iter"] == warm + args.steps and st["done"] == 0, st
     points = s.interior_points
     value = points * args.steps / dt / 1e9
     esize = 8 if args.dtype == "fp64" else 4
     kernel = s.kernel
     comm_name = s.native.comm_name
+    comm_ranks = s.native.comm_transport_ranks
+    K = s.native.temporal_steps
+    nbuf = s.native.field_buffers
+    placement = all_gather_objects({"rank": rank, "device": dev, "host": socket.gethostname(),
+                                    "subdomain": list(s.native.local_subdomain(0)["n"])}, group)
     del s
 
     ttc = None
@@ -134,8 +243,11 @@ def main() -> int:
         del c
 
     par = "x".join(str(d) for d in dims)
+    grid_txt = "x".join(map(str, N)) if len(set(N)) > 1 else f"{G}^3"
+    metric = metric_name(grid_txt, args.dtype)
+    is_headline = metric == BASELINE_METRIC and args.virtual_ranks == 1 and not args.weak_block
     out = {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(value, 3),
         "unit": "GLUPS",
         "n_gpus": world,
@@ -147,17 +259,27 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (analytic Dirichlet IC/BC of the reference, random-free)",
-        "config": {"model": f"heat3d FTCS 7-point, {'x'.join(map(str, N)) if len(set(N)) > 1 else f'{G}^3'} {args.dtype} grid",
+        "config": {"model": f"heat3d FTCS 7-point, {grid_txt} {args.dtype} grid",
                    "grid": list(N),
-                   "global_batch": 1, "seq_len": G, "parallelism": f"{'slab' if dims[1] == dims[2] == 1 and dims[0] > 1 else 'block'} {par}"
+                   "global_batch": 1, "seq_len": G,
+                   "parallelism": f"{'slab' if dims[1] == dims[2] == 1 and dims[0] > 1 else 'block'} {par}"
                    + (f" ({args.virtual_ranks} virtual ranks on 1 GPU)" if args.virtual_ranks > 1 else ""),
-                   "kernel": kernel, "graph": not args.no_graph, "overlap": not args.no_overlap,
-                   "comm": comm_name},
+                   "kernel": kernel, "temporal_K": K, "field_buffers": nbuf,
+                   "graph_requested": not args.no_graph, "graph_used": graph_launches > 0,
+                   "graph_launches": graph_launches,
+                   "overlap": not args.no_overlap, "comm": comm_name},
+        "comm_ranks": comm_ranks,
+        "placement": placement,
+        "halo_verified": True,
+        "headline_config": is_headline,
         "glups_per_gpu": round(value / world, 3),
-        "effective_hbm_tbps_per_gpu": round(value / world * 2 * esize / 1e3, 3),
-        "vs_roofline": round(value / roofline_glups(esize, world), 4),
+        # the single-step-equivalent traffic rate (16 B / 8 B per point update);
+        # the real HBM traffic is about 1/K of it with K-step temporal blocking
+        "single_step_equiv_tbps_per_gpu": round(value / world * 2 * esize / 1e3, 3),
+        "vs_single_step_roofline": round(value / roofline_glups(esize, world), 4),
         "time_to_converge": ttc,
-        "baseline_note": "reference publishes no numbers (BASELINE.md); roofline = 6.29 TB/s / (2*esize) per GPU",
+        "baseline_note": "reference publishes no numbers (BASELINE.md); single-step roofline = "
+                         "6.29 TB/s / (2*esize) per GPU",
     }
     if rank == 0:
         line = json.dumps(out)
@@ -168,8 +290,18 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist
 
+        barrier(group)
         dist.destroy_process_group()
     return 0
+
+
+def main() -> int:
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the ranks ourselves (nothing here has touched HIP)
+        return launch(args, argv)
+    return run_rank(args)
 
 
 if __name__ == "__main__":

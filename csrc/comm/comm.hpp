@@ -52,6 +52,14 @@ class Comm {
   // True when all ranks live in this process and share one DeviceState
   // (no reduction needed, halos are direct copies).
   virtual bool all_local() const { return false; }
+  // Ranks as counted by the transport itself (RCCL: ncclCommCount), so a run
+  // report can prove the communicator really spans the job.
+  virtual int transport_ranks() const { return size(); }
+  // True when exchange() and allreduce() are device-side collectives of one
+  // job-wide ordering domain (RCCL): the solver then chains every such call
+  // behind the previous one with events, so all ranks' GPUs execute them in
+  // one identical total order (see Solver::comm_token_*).
+  virtual bool ordered_collectives() const { return false; }
 
   virtual void exchange(const std::vector<Transfer>& xs, Backend& be, StreamId s) = 0;
   virtual void allreduce(void* buf, std::size_t count, RedType t, RedOp op, Backend& be,

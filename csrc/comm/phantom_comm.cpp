@@ -5,10 +5,15 @@
 // boundary kernels, deep halos, streams, lagged all-reduce), while the peers
 // are phantoms.  Received halos are filled with a same-sized face this rank
 // sends (numerically meaningless, finite), every exchange occupies the stream
-// for bytes-per-peer / HEAT3D_PHANTOM_GBPS (a one-workgroup delay kernel — an
-// RCCL p2p kernel also holds a CU while it moves data), and every all-reduce
-// for HEAT3D_PHANTOM_ALLREDUCE_US.  This is how the per-GPU time of the
-// multi-GPU bench is measured on the one-GPU box (tools/rank_proxy.py).
+// for bytes-per-peer / HEAT3D_PHANTOM_GBPS, and every all-reduce for
+// HEAT3D_PHANTOM_ALLREDUCE_US.  Like RCCL, which moves p2p data with several
+// channels (one workgroup each) per peer, the emulated transfer holds
+// HEAT3D_PHANTOM_CHANNELS workgroups per peer (default 4) for its duration, and
+// the all-reduce one per ring channel (default 2): those workgroups must find
+// free CUs next to the interior sweep, exactly the contention a real run has.
+// Collectives are ordered like RCCL's (ordered_collectives).  This is how the
+// per-GPU time of the multi-GPU bench is measured on the one-GPU box
+// (tools/rank_proxy.py).
 #include <cstdlib>
 #include <map>
 
@@ -27,7 +32,9 @@ class PhantomComm final : public Comm {
  public:
   PhantomComm(int rank, int size)
       : rank_(rank), size_(size), gbps_(env_or("HEAT3D_PHANTOM_GBPS", 50.0)),
-        ar_us_(env_or("HEAT3D_PHANTOM_ALLREDUCE_US", 20.0)) {
+        ar_us_(env_or("HEAT3D_PHANTOM_ALLREDUCE_US", 20.0)),
+        channels_((int)env_or("HEAT3D_PHANTOM_CHANNELS", 4)),
+        ar_channels_((int)env_or("HEAT3D_PHANTOM_ALLREDUCE_CHANNELS", 2)) {
     HEAT3D_CHECK(rank >= 0 && rank < size, "phantom rank " << rank << " of " << size);
   }
   const char* name() const override { return "phantom"; }
@@ -35,6 +42,7 @@ class PhantomComm final : public Comm {
   std::vector<int> local_ranks() const override { return {rank_}; }
   bool device_buffers() const override { return true; }
   bool capturable() const override { return true; }
+  bool ordered_collectives() const override { return true; }
 
   void exchange(const std::vector<Transfer>& xs, Backend& be, StreamId s) override {
     std::map<int, std::size_t> per_peer;
@@ -42,7 +50,8 @@ class PhantomComm final : public Comm {
       if (x.dst_rank == rank_ && x.src_rank != rank_) per_peer[x.src_rank] += x.bytes;
     std::size_t worst = 0;
     for (const auto& kv : per_peer) worst = std::max(worst, kv.second);
-    if (worst && gbps_ > 0) be.delay(worst / (gbps_ * 1e3), s);  // bytes / (GB/s) in us
+    // bytes / (GB/s) in us, every peer's channels in flight at once
+    if (worst && gbps_ > 0) be.delay(worst / (gbps_ * 1e3), s, channels_ * (int)per_peer.size());
     for (const auto& x : xs) {
       if (x.dst_rank != rank_ || x.src_rank == rank_) continue;
       const void* src = nullptr;
@@ -52,7 +61,7 @@ class PhantomComm final : public Comm {
     }
   }
   void allreduce(void*, std::size_t, RedType, RedOp, Backend& be, StreamId s) override {
-    if (ar_us_ > 0) be.delay(ar_us_, s);
+    if (ar_us_ > 0) be.delay(ar_us_, s, ar_channels_);
   }
   void send(const void*, std::size_t, int, Backend&, StreamId) override {}
   void recv(void*, std::size_t, int, Backend&, StreamId) override {}
@@ -61,6 +70,7 @@ class PhantomComm final : public Comm {
  private:
   int rank_, size_;
   double gbps_, ar_us_;
+  int channels_, ar_channels_;
 };
 
 }  // namespace

@@ -4,14 +4,30 @@
 // 1037-1063) with device-pointer RCCL calls enqueued on HIP streams:
 //   * halo: ncclGroupStart; ncclSend/ncclRecv per neighbour face; ncclGroupEnd
 //     (x faces are contiguous planes sent in place — no pack);
-//   * convergence: ncclAllReduce(max) on the 8-byte residual word, on a second
-//     communicator (ncclCommSplit) so it never serialises behind halo traffic;
+//   * convergence: ncclAllReduce(max) on the 8-byte residual words, on a second
+//     communicator (ncclCommSplit) so that it does not queue behind halo traffic
+//     inside RCCL's per-communicator stream ordering;
 //   * failure detection: ncclCommGetAsyncError polling, ncclCommAbort on fault.
 // On a fully connected 8x MI355X node every face neighbour is one direct xGMI
 // link, so a slab drives 2 links per GPU and a 2x2x2 block 3.
+//
+// Ordering contract (why two communicators on two streams cannot deadlock or
+// mismatch).  NCCL requires that every rank issue a communicator's operations
+// in one order, and gives no order between operations of different
+// communicators running on different streams.  The solver therefore never
+// relies on the GPU's choice: it chains every collective it enqueues (halo
+// group or all-reduce) behind the previous one with an event
+// (Solver::comm_token_wait / comm_token_signal), and issues them in the same
+// host order on every rank.  Each rank's GPU executes the collectives in one
+// total order, identical across ranks, with at most one in flight.  The
+// overlapped sweeps issue all-reduce(q) after halo(q+1) (Solver::enqueue_multi),
+// so the chain costs the next halo nothing.  If ncclCommSplit is unavailable
+// both kinds share one communicator: RCCL then serialises them in host issue
+// order, which is the same total order.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -52,6 +68,19 @@ ncclDataType_t to_nccl(RedType t) {
   return ncclUint64;
 }
 
+// Element type and count of a byte message: 8-byte words when the size allows
+// (fewer, wider elements for RCCL's copy loops), else bytes.  Both sides of a
+// transfer compute the same pair from the same byte count.
+void message_shape(std::size_t bytes, ncclDataType_t* dt, std::size_t* count) {
+  if (bytes % 8 == 0) {
+    *dt = ncclUint64;
+    *count = bytes / 8;
+  } else {
+    *dt = ncclUint8;
+    *count = bytes;
+  }
+}
+
 class RcclComm final : public Comm {
  public:
   RcclComm(int rank, int size, const std::string& uid, int device) : rank_(rank), size_(size) {
@@ -60,10 +89,14 @@ class RcclComm final : public Comm {
     std::memcpy(&id, uid.data(), sizeof(id));
     if (hipSetDevice(device) != hipSuccess) HEAT3D_THROW("hipSetDevice(" << device << ") failed");
     NCCL_CHECK(ncclCommInitRank(&halo_, size_, id, rank_));
-    // A second communicator for the per-iteration scalar all-reduce; if the
-    // runtime RCCL cannot split, reductions share the halo communicator
-    // (still correct: every rank issues both streams' ops in one order).
-    if (ncclCommSplit(halo_, 0, rank_, &red_, nullptr) != ncclSuccess || red_ == nullptr) {
+    int n = 0;
+    NCCL_CHECK(ncclCommCount(halo_, &n));
+    HEAT3D_CHECK(n == size_, "RCCL communicator has " << n << " ranks, expected " << size_);
+    // A second communicator for the scalar all-reduce (HEAT3D_RCCL_SHARED=1
+    // forces the single-communicator form, which tests exercise).
+    const char* e = std::getenv("HEAT3D_RCCL_SHARED");
+    const bool force_shared = e && e[0] == '1';
+    if (force_shared || ncclCommSplit(halo_, 0, rank_, &red_, nullptr) != ncclSuccess || red_ == nullptr) {
       red_ = halo_;
       shared_ = true;
     }
@@ -73,23 +106,34 @@ class RcclComm final : public Comm {
     if (red_ && !shared_) ncclCommDestroy(red_);
     if (halo_) ncclCommDestroy(halo_);
   }
-  const char* name() const override { return "rccl"; }
+  const char* name() const override { return shared_ ? "rccl(shared)" : "rccl"; }
   int size() const override { return size_; }
   std::vector<int> local_ranks() const override { return {rank_}; }
   bool device_buffers() const override { return true; }
-  bool capturable() const override { return true; }
+  // RCCL kernels inside a hipGraph capture have not been validated on this
+  // stack: graphs are refused unless HEAT3D_RCCL_GRAPH=1.
+  bool capturable() const override {
+    const char* e = std::getenv("HEAT3D_RCCL_GRAPH");
+    return e && e[0] == '1';
+  }
+  int transport_ranks() const override {
+    int n = 0;
+    if (!halo_ || ncclCommCount(halo_, &n) != ncclSuccess) return -1;
+    return n;
+  }
+  bool ordered_collectives() const override { return true; }
 
   void exchange(const std::vector<Transfer>& xs, Backend& be, StreamId s) override {
     hipStream_t st = static_cast<hipStream_t>(be.stream(s));
     NCCL_CHECK(ncclGroupStart());
     for (const auto& x : xs) {
-      const bool w8 = (x.bytes % 8) == 0;
-      const std::size_t cnt = w8 ? x.bytes / 8 : x.bytes;
-      const ncclDataType_t dt = w8 ? ncclUint64 : ncclUint8;
-      if (x.src_rank == rank_ && x.dst_rank != rank_)
-        NCCL_CHECK(ncclSend(x.src, cnt, dt, x.dst_rank, halo_, st));
-      else if (x.dst_rank == rank_ && x.src_rank != rank_)
-        NCCL_CHECK(ncclRecv(x.dst, cnt, dt, x.src_rank, halo_, st));
+      ncclDataType_t dt;
+      std::size_t cnt;
+      message_shape(x.bytes, &dt, &cnt);
+      // a transfer between two faces of this rank (periodic self-neighbour or
+      // the 1-rank test) is a send and a receive to itself inside the group
+      if (x.src_rank == rank_) NCCL_CHECK(ncclSend(x.src, cnt, dt, x.dst_rank, halo_, st));
+      if (x.dst_rank == rank_) NCCL_CHECK(ncclRecv(x.dst, cnt, dt, x.src_rank, halo_, st));
     }
     NCCL_CHECK(ncclGroupEnd());
   }
@@ -101,11 +145,17 @@ class RcclComm final : public Comm {
   }
   void send(const void* buf, std::size_t bytes, int peer, Backend& be, StreamId s) override {
     hipStream_t st = static_cast<hipStream_t>(be.stream(s));
-    NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, halo_, st));
+    ncclDataType_t dt;
+    std::size_t cnt;
+    message_shape(bytes, &dt, &cnt);
+    NCCL_CHECK(ncclSend(buf, cnt, dt, peer, halo_, st));
   }
   void recv(void* buf, std::size_t bytes, int peer, Backend& be, StreamId s) override {
     hipStream_t st = static_cast<hipStream_t>(be.stream(s));
-    NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, halo_, st));
+    ncclDataType_t dt;
+    std::size_t cnt;
+    message_shape(bytes, &dt, &cnt);
+    NCCL_CHECK(ncclRecv(buf, cnt, dt, peer, halo_, st));
   }
   void barrier(Backend& be) override {
     if (!bar_ && hipMalloc(&bar_, 8) != hipSuccess) HEAT3D_THROW("hipMalloc failed");

@@ -90,8 +90,9 @@ void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf
 void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
               const Layout& Ld, const Box& bd, void* stream);
 void check_convergence(DeviceState* s, int slot, void* stream, int count = 1);
-// one-lane kernel spinning for `us` microseconds on the 100 MHz real-time clock
-void delay(double us, void* stream);
+// kernel of `blocks` one-wave workgroups spinning for `us` microseconds on the
+// 100 MHz real-time clock (each holds a wave slot of one CU while it spins)
+void delay(double us, void* stream, int blocks = 1);
 // Adds Σ|T - y| and the point count over `box` into s->error_sum/error_count.
 // `scratch` must hold at least error_scratch_elems() doubles.
 void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,

@@ -555,9 +555,10 @@ static void launch_tile(const StencilParams& p, const KernelSpec& k, hipStream_t
   g.nyb = (int)((b.extent(1) + (int64_t)R * WY - 1) / ((int64_t)R * WY));
   int seg = k.L;
   if (seg <= 0) {
-    static int slots = 0;  // resident workgroups on the whole device (cached per instantiation)
-    if (!slots) slots = device_slots(reinterpret_cast<const void*>(&stencil_tile<Real, V, R, WZ, WY>),
-                                     64 * WZ * WY);
+    // resident workgroups on the whole device, once per instantiation (a
+    // magic static: thread-safe under --gpus N's host thread per GPU)
+    static const int slots = device_slots(reinterpret_cast<const void*>(&stencil_tile<Real, V, R, WZ, WY>),
+                                          64 * WZ * WY);
     seg = choose_segment(b.extent(0), (int64_t)g.nzb * g.nyb, slots);
   }
   g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));
@@ -793,9 +794,10 @@ __global__ void delay_kernel(unsigned long long ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
-void delay(double us, void* stream) {
+void delay(double us, void* stream, int blocks) {
   if (us <= 0) return;
-  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, S(stream), (unsigned long long)(us * 100.0));
+  hipLaunchKernelGGL(delay_kernel, dim3((unsigned)std::max(1, blocks)), dim3(64), 0, S(stream),
+                     (unsigned long long)(us * 100.0));
   HIPK_CHECK(hipGetLastError());
 }
 

@@ -281,9 +281,8 @@ static void launch_tb2(const StencilParams& p, const KernelSpec& k, hipStream_t 
   g.nyb = (int)std::max<int64_t>(1, (yspan + (TYB - 2) - 1) / (TYB - 2));
   int seg = k.L;
   if (seg <= 0) {
-    static int slots = 0;
-    if (!slots) slots = device_slots(reinterpret_cast<const void*>(&stencil_tb2<Real, V, R, WZ, WY>),
-                                     64 * WZ * WY);
+    static const int slots = device_slots(reinterpret_cast<const void*>(&stencil_tb2<Real, V, R, WZ, WY>),
+                                          64 * WZ * WY);  // magic static: thread-safe
     seg = choose_segment(b.extent(0), (int64_t)g.nzb * g.nyb, slots, 4);
   }
   g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));

@@ -368,9 +368,8 @@ static void launch_tbk(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + ystep - 1) / ystep);
   int seg = ks.L;
   if (seg <= 0) {
-    static int slots = 0;
-    if (!slots)
-      slots = device_slots(reinterpret_cast<const void*>(&stencil_tbk<Real, V, R, WZ, WY, K, PD>), 64 * WZ * WY);
+    static const int slots =  // magic static: thread-safe
+        device_slots(reinterpret_cast<const void*>(&stencil_tbk<Real, V, R, WZ, WY, K, PD>), 64 * WZ * WY);
     seg = choose_segment(b.extent(0), (int64_t)g.nzb * g.nyb, slots, 2 * K);
   }
   g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));

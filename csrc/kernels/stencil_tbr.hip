@@ -433,9 +433,8 @@ static void launch_tbr(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.nzb = (int)std::max<int64_t>(1, (zspan + g.zstep - 1) / g.zstep);
   const int ystep = TYB - 2 * (K - 1);
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + ystep - 1) / ystep);
-  static int slots = 0;
-  if (!slots)
-    slots = device_slots(reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q, NTS>), 64 * WY);
+  static const int slots =  // magic static: thread-safe under --gpus N
+      device_slots(reinterpret_cast<const void*>(&stencil_tbr<Real, V, R, WY, K, Q, NTS>), 64 * WY);
   const int64_t ntiles = (int64_t)g.nzb * g.nyb;
   const int64_t nxb = b.extent(0);
   constexpr int U = Q == 3 ? 3 : 12;  // a piece runs its steps in chunks of U = lcm(Q, 3)

@@ -168,6 +168,108 @@ PYBIND11_MODULE(_heat3d, m) {
   m.def("device_count", &hip_device_count);
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
+  // Executes RcclComm::exchange / allreduce on a one-rank communicator: every
+  // transfer is a send and a receive to self inside one RCCL group (sizes that
+  // are and are not multiples of 8 bytes), plus a padded K-deep x halo plane of
+  // a ghosted Layout moved in place between two fields, as the solver sends
+  // x faces.  Returns per-transfer byte equality and the all-reduce results.
+  m.def("rccl_self_exchange", [](int device, std::vector<int64_t> sizes, std::array<int64_t, 3> n, int depth) {
+    auto be = make_hip_backend(device);
+    auto comm = make_rccl_comm(0, 1, rccl_unique_id(), device);
+    std::vector<Transfer> xs;
+    std::vector<std::vector<unsigned char>> want;
+    std::vector<void*> dsts, bufs;
+    auto pattern = [](std::size_t bytes, unsigned seed) {
+      std::vector<unsigned char> h(bytes);
+      for (std::size_t i = 0; i < bytes; ++i) h[i] = (unsigned char)((i * 131u + seed * 17u + (i >> 8)) & 0xff);
+      return h;
+    };
+    for (std::size_t q = 0; q < sizes.size(); ++q) {
+      const std::size_t b = (std::size_t)sizes[q];
+      void* src = be->alloc(b);
+      void* dst = be->alloc(b);
+      auto h = pattern(b, (unsigned)q + 1);
+      be->copy(src, h.data(), b, CopyKind::H2D, kComm);
+      be->memset(dst, 0xEE, b, kComm);
+      be->sync(kComm);
+      Transfer t;
+      t.src_rank = t.dst_rank = 0;
+      t.src = src;
+      t.dst = dst;
+      t.bytes = b;
+      xs.push_back(t);
+      want.push_back(h);
+      dsts.push_back(dst);
+      bufs.push_back(src);
+      bufs.push_back(dst);
+    }
+    // padded x halo: planes [n0-depth, n0) of field A into ghost planes
+    // [-depth, 0) of field B, whole planes (ghost rows and row padding included)
+    int64_t nn[3] = {n[0], n[1], n[2]};
+    const Layout L = Layout::make(nn, 8, depth, 1, 1);
+    void* fa = be->alloc(L.bytes());
+    void* fb = be->alloc(L.bytes());
+    auto ha = pattern(L.bytes(), 99);
+    be->copy(fa, ha.data(), L.bytes(), CopyKind::H2D, kComm);
+    be->memset(fb, 0xEE, L.bytes(), kComm);
+    be->sync(kComm);
+    const std::size_t pb = (std::size_t)(depth * L.sx * 8);
+    Transfer t;
+    t.src_rank = t.dst_rank = 0;
+    t.src = static_cast<char*>(fa) + L.plane_offset(n[0] - depth) * 8;
+    t.dst = static_cast<char*>(fb) + L.plane_offset(-depth) * 8;
+    t.bytes = pb;
+    xs.push_back(t);
+    want.emplace_back(ha.begin() + L.plane_offset(n[0] - depth) * 8, ha.begin() + L.plane_offset(n[0] - depth) * 8 + pb);
+    dsts.push_back(t.dst);
+    comm->exchange(xs, *be, kComm);
+    be->sync(kComm);
+    comm->check_async_error();
+    py::list ok;
+    for (std::size_t q = 0; q < xs.size(); ++q) {
+      std::vector<unsigned char> got(xs[q].bytes);
+      be->copy(got.data(), dsts[q], xs[q].bytes, CopyKind::D2H, kComm);
+      be->sync(kComm);
+      ok.append(got == want[q]);
+    }
+    // the planes around the halo must be untouched
+    std::vector<unsigned char> whole(L.bytes());
+    be->copy(whole.data(), fb, L.bytes(), CopyKind::D2H, kComm);
+    be->sync(kComm);
+    std::size_t touched = 0;
+    const std::size_t h0 = (std::size_t)L.plane_offset(-depth) * 8;
+    for (std::size_t i = 0; i < whole.size(); ++i)
+      if (i < h0 || i >= h0 + pb) touched += whole[i] != 0xEE;
+    // all-reduce on one rank: max of u64 words and sum of doubles are identities
+    unsigned long long hu[3] = {7ull, 0x7ff0000000000000ull, 3ull};
+    double hd[2] = {1.5, -2.25};
+    void* du = be->alloc(sizeof(hu));
+    void* dd = be->alloc(sizeof(hd));
+    be->copy(du, hu, sizeof(hu), CopyKind::H2D, kReduce);
+    be->copy(dd, hd, sizeof(hd), CopyKind::H2D, kReduce);
+    comm->allreduce(du, 3, RedType::U64, RedOp::Max, *be, kReduce);
+    comm->allreduce(dd, 2, RedType::F64, RedOp::Sum, *be, kReduce);
+    unsigned long long ru[3];
+    double rd[2];
+    be->copy(ru, du, sizeof(ru), CopyKind::D2H, kReduce);
+    be->copy(rd, dd, sizeof(rd), CopyKind::D2H, kReduce);
+    be->sync(kReduce);
+    py::dict d;
+    d["ok"] = ok;
+    d["plane_bytes"] = pb;
+    d["touched_outside"] = touched;
+    d["allreduce_u64"] = py::make_tuple(ru[0], ru[1], ru[2]);
+    d["allreduce_f64"] = py::make_tuple(rd[0], rd[1]);
+    d["transport_ranks"] = comm->transport_ranks();
+    d["name"] = std::string(comm->name());
+    for (void* p : bufs) be->release(p);
+    be->release(fa);
+    be->release(fb);
+    be->release(du);
+    be->release(dd);
+    comm.reset();
+    return d;
+  }, py::arg("device"), py::arg("sizes"), py::arg("n") = std::array<int64_t, 3>{6, 7, 9}, py::arg("depth") = 3);
   m.def("socket_listen", []() {
     int port = 0;
     int fd = net::listen_on("0.0.0.0", 0, &port);
@@ -441,6 +543,10 @@ PYBIND11_MODULE(_heat3d, m) {
         py::gil_scoped_release nogil;
         s.synchronize();
       })
+      .def("prepare_steps", [](Solver& s, int64_t n) {
+        py::gil_scoped_release nogil;
+        s.prepare_steps(n);
+      })
       .def("state", [](Solver& s) {
         HostState h = s.state();
         py::dict d;
@@ -503,6 +609,9 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("process_rank", &Solver::process_rank)
       .def_property_readonly("interior_points", &Solver::interior_points)
       .def_property_readonly("iterations_issued", &Solver::iterations_issued)
+      .def_property_readonly("graph_launches", &Solver::graph_launches)
+      .def_property_readonly("comm_transport_ranks", [](Solver& s) { return s.comm().transport_ranks(); })
+      .def_property_readonly("device", [](Solver& s) { return s.backend().device(); })
       .def_property_readonly("kernel_name", &Solver::kernel_name)
       .def_property_readonly("temporal_blocking", &Solver::temporal_blocking)
       .def_property_readonly("temporal_steps", &Solver::temporal_steps)

@@ -77,9 +77,9 @@ class Backend {
   // order-independent checksum of a box into *out (device memory on HIP)
   virtual void box_bitsum(DType t, const void* f, const Layout& L, const Box& b,
                           unsigned long long* out, StreamId s) = 0;
-  // diagnostic: occupy stream s for `us` microseconds (emulated collective
-  // latency, HEAT3D_FAKE_ALLREDUCE_US); no-op on the CPU
-  virtual void delay(double /*us*/, StreamId /*s*/) {}
+  // diagnostic: occupy stream s for `us` microseconds with `blocks` spinning
+  // workgroups (emulated collective latency / transfer time); no-op on the CPU
+  virtual void delay(double /*us*/, StreamId /*s*/, int /*blocks*/ = 1) {}
   // tracing ranges (roctx on HIP)
   virtual void range_push(const char* /*name*/) {}
   virtual void range_pop() {}

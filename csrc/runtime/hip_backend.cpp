@@ -171,7 +171,7 @@ class HipBackend final : public Backend {
                 const Layout& Ld, const Box& bd, StreamId s) override {
     hip::copy_box(t, src, Ls, bs, dst, Ld, bd, streams_[s]);
   }
-  void delay(double us, StreamId s) override { hip::delay(us, streams_[s]); }
+  void delay(double us, StreamId s, int blocks) override { hip::delay(us, streams_[s], blocks); }
   void check_convergence(DeviceState* st, int slot, StreamId s, int count) override {
     hip::check_convergence(st, slot, streams_[s], count);
   }

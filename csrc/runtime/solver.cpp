@@ -195,6 +195,7 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   }
   nbuf_ = lag_ ? 3 : 2;
   if (const char* e = std::getenv("HEAT3D_FAKE_ALLREDUCE_US")) fake_allreduce_us_ = std::atof(e);
+  chain_ = comm_->ordered_collectives() && !comm_->all_local() && comm_->size() > 1;
 
   for (int r : comm_->local_ranks()) {
     Local l;
@@ -258,7 +259,7 @@ Solver::~Solver() {
     be_->sync_all();
   } catch (...) {
   }
-  if (graph_) be_->destroy_graph(graph_);
+  destroy_graphs();
   for (auto& e : ev_)
     if (e) be_->event_destroy(e);
   for (auto& e : cap_pool_) be_->event_destroy(e);
@@ -368,10 +369,8 @@ void Solver::ev_wait(StreamId s, int id) {
 
 void Solver::initialize() {
   be_->sync_all();
-  if (graph_) {
-    be_->destroy_graph(graph_);
-    graph_ = nullptr;
-  }
+  destroy_graphs();
+  pending_.valid = false;
   for (auto& l : local_) {
     InitParams p = init_params(l);
     for (int b = 0; b < nbuf_; ++b) {
@@ -455,7 +454,11 @@ void Solver::enqueue_halo_phase(int p, StreamId s, Pred in_phase) {
         xs.push_back(rcv);
       }
     }
-    if (!xs.empty()) comm_->exchange(xs, *be_, s);
+    if (!xs.empty()) {
+      comm_token_wait(s);
+      comm_->exchange(xs, *be_, s);
+      comm_token_signal(s);
+    }
     for (auto& l : local_)
       for (auto& io : l.faces)
         if (in_phase(io) && !io.contiguous) be_->unpack_box(dt_, l.field[p], l.L, io.recv_box, io.recvbuf, s);
@@ -536,9 +539,7 @@ void Solver::enqueue_iteration(int p, int bi) {
   ev_wait(kReduce, EV_INT + p);
   if (overlap_) ev_wait(kReduce, EV_BND + p);
   T(5, kReduce);
-  if (!comm_->all_local() && comm_->size() > 1)
-    comm_->allreduce(&dstate_->residual[p], 1, RedType::U64, RedOp::Max, *be_, kReduce);
-  be_->check_convergence(dstate_, p, kReduce);
+  reduce_and_check(kReduce, p, 1);
   T(6, kReduce);
   ev_record(EV_CHK + p, kReduce);
 }
@@ -596,13 +597,6 @@ void Solver::enqueue_multi(int bi, int Kp) {
     shrink(l.uz, l.sd.n[2], sp.uz);
     return sp;
   };
-  auto reduce_and_check = [&](StreamId s) {
-    if (!comm_->all_local() && comm_->size() > 1)
-      comm_->allreduce(&dstate_->residual[slot0], Kp, RedType::U64, RedOp::Max, *be_, s);
-    else if (fake_allreduce_us_ > 0)
-      be_->delay(fake_allreduce_us_, s);  // single-GPU stand-in for the RCCL latency
-    be_->check_convergence(dstate_, slot0, s, Kp);
-  };
   if (!tb_overlap_) {
     ev_wait(kCompute, EV_CHK + 0);
     ev_wait(kCompute, EV_CHK + 1);
@@ -610,7 +604,7 @@ void Solver::enqueue_multi(int bi, int Kp) {
     be_->range_push("sweep");
     for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), ks, kCompute);
     be_->range_pop();
-    reduce_and_check(kCompute);
+    reduce_and_check(kCompute, slot0, Kp);
     if (!capturing_) {
       for (int i = 0; i < 2; ++i) {
         ev_record(EV_INT + i, kCompute);
@@ -637,6 +631,10 @@ void Solver::enqueue_multi(int bi, int Kp) {
   ev_record(EV_INT + q, kCompute);
   // [B] deep halo, then the boundary slabs
   enqueue_halo(bi, kComm);
+  // the previous sweep's all-reduce follows this halo in the collective
+  // chain: the halo of sweep q depends only on the boundary slabs of q-1 and
+  // must not queue behind the all-reduce of q-1, which waits for its interior
+  flush_pending_reduce();
   ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
   ev_wait(kComm, EV_CHK + chk_prev);
   be_->range_push("boundary");
@@ -644,17 +642,52 @@ void Solver::enqueue_multi(int bi, int Kp) {
     for (const Box& b : l.tb_boundary) be_->stencil2(dt_, params(l, b), ks, kComm);
   be_->range_pop();
   ev_record(EV_BND + q, kComm);
-  // [C] all residuals, all checks
-  ev_wait(kReduce, EV_INT + q);
-  ev_wait(kReduce, EV_BND + q);
-  reduce_and_check(kReduce);
-  ev_record(EV_CHK + q, kReduce);
+  // [C] all residuals, all checks: now, or (lagged, ordered collectives) after
+  // the next sweep's halo.  Nothing waits for CHK(q) before sweep q+2 (with the
+  // lag), whose halo is issued after that point, so deferring costs nothing.
+  pending_.valid = true;
+  pending_.q = q;
+  pending_.slot0 = slot0;
+  pending_.Kp = Kp;
+  if (!(lag_ && chain_)) flush_pending_reduce();
   ++nsweep_;
 }
 
+void Solver::reduce_and_check(StreamId s, int slot0, int Kp) {
+  if (!comm_->all_local() && comm_->size() > 1) {
+    comm_token_wait(s);
+    comm_->allreduce(&dstate_->residual[slot0], Kp, RedType::U64, RedOp::Max, *be_, s);
+    comm_token_signal(s);
+  } else if (fake_allreduce_us_ > 0) {
+    be_->delay(fake_allreduce_us_, s);  // single-GPU stand-in for the RCCL latency
+  }
+  be_->check_convergence(dstate_, slot0, s, Kp);
+}
+
+void Solver::flush_pending_reduce() {
+  if (!pending_.valid) return;
+  pending_.valid = false;
+  const int q = pending_.q;
+  ev_wait(kReduce, EV_INT + q);
+  ev_wait(kReduce, EV_BND + q);
+  reduce_and_check(kReduce, pending_.slot0, pending_.Kp);
+  ev_record(EV_CHK + q, kReduce);
+}
+
+void Solver::comm_token_wait(StreamId s) {
+  if (chain_) ev_wait(s, EV_TOKEN);
+}
+
+void Solver::comm_token_signal(StreamId s) {
+  if (chain_) ev_record(EV_TOKEN, s);
+}
+
 void Solver::join_pipeline() {
-  for (StreamId s : {kCompute, kComm, kReduce})
+  flush_pending_reduce();
+  for (StreamId s : {kCompute, kComm, kReduce}) {
     for (int id = EV_INT; id < EV_CHK + 2; ++id) ev_wait(s, id);
+    ev_wait(s, EV_TOKEN);
+  }
 }
 
 void Solver::record_segment(int64_t start, int len, int inbuf) {
@@ -721,20 +754,68 @@ void Solver::accumulate_phase_times() {
   ++phase_count_;
 }
 
-void Solver::build_graph() {
-  H3D_TRACE("build_graph at issued=" << issued_);
-  // G iterations per graph; temporally blocked graphs hold an even number of
-  // pairs so that the buffer roles repeat (G multiple of 4)
-  int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
-  if (tb_) G = std::max(2 * K_, G - (G % (2 * K_)));
-  graph_kind_ = tb_ ? 2 : 1;
-  graph_parity_ = (int)(issued_ & 1);
-  graph_buf_ = cur();
+// Iterations per captured graph for a chunk of n: --graph-chunk, or the
+// largest whole number of schedule cycles <= n, so that a short run (the
+// driver's 20-step bench) replays a graph too.  A cycle brings every rotating
+// role back to its start: the buffer ring (2, or 3 with the lagged check), the
+// event / residual-slot parity of single steps (2) and of overlapped sweeps (2).
+int Solver::graph_len_for(int64_t n) const {
+  int cyc;
+  if (tb_) cyc = K_ * (nbuf_ == 3 ? 6 : 2);
+  else cyc = nbuf_ == 3 ? 6 : 2;
+  int G = std::max(cyc, cfg_.graph_chunk - cfg_.graph_chunk % cyc);
+  if (n < G) G = (int)(n - n % cyc);
+  return G;
+}
+
+bool Solver::graphs_allowed() const {
+  // Multi-stream (overlapped) schedules: HEAT3D_GRAPH_MULTISTREAM=1 (capture of
+  // the three-stream fork/join crashes in the HIP runtime, docs/ARCHITECTURE.md)
+  static const bool ms_ok = [] {
+    const char* e = std::getenv("HEAT3D_GRAPH_MULTISTREAM");
+    return e && e[0] == '1';
+  }();
+  return cfg_.use_graph && be_->supports_graphs() && comm_->capturable() && !graph_failed_ && !phase_timing_ &&
+         (!multi_stream() || ms_ok);
+}
+
+Solver::GraphEntry* Solver::find_graph(int G) {
+  const int kind = tb_ ? 2 : 1;
+  for (auto& g : graphs_)
+    if (g.exec && g.G == G && g.kind == kind && g.buf == cur() && g.parity == (int)(issued_ & 1) &&
+        g.sparity == (int)(nsweep_ & 1))
+      return &g;
+  return nullptr;
+}
+
+void Solver::destroy_graphs() {
+  if (graphs_.empty()) return;
+  be_->sync_all();
+  for (auto& g : graphs_) be_->destroy_graph(g.exec);
+  graphs_.clear();
+}
+
+// Capture G iterations, as run_chunk would issue them eagerly from the current
+// state, into one graph on the compute stream; the comm / reduce streams fork
+// from it and join back into it (fresh events for every record inside the
+// capture).  The solver's host-side schedule state is restored afterwards: a
+// launch advances it exactly like the eager path.
+Solver::GraphEntry* Solver::build_graph(int G) {
+  H3D_TRACE("build_graph G=" << G << " at issued=" << issued_);
+  join_pipeline();
+  GraphEntry e;
+  e.G = G;
+  e.kind = tb_ ? 2 : 1;
+  e.buf = cur();
+  e.parity = (int)(issued_ & 1);
+  e.sparity = (int)(nsweep_ & 1);
   bool saved[EV_COUNT];
   std::memcpy(saved, ev_valid_, sizeof(saved));
   Event saved_cur[EV_COUNT];
   std::memcpy(saved_cur, cur_ev_, sizeof(saved_cur));
-  const std::size_t need = 8 * (std::size_t)G + 8;
+  const int64_t s_issued = issued_, s_nsweep = nsweep_;
+  const int s_cur = cur_, s_last = last_kind_;
+  const std::size_t need = 16 * (std::size_t)G + 16;
   while (cap_pool_.size() < need) cap_pool_.push_back(be_->event_create());
   cap_next_ = 0;
   try {
@@ -744,81 +825,95 @@ void Solver::build_graph() {
     ev_record(EV_FORK, kCompute);
     ev_wait(kComm, EV_FORK);
     ev_wait(kReduce, EV_FORK);
-    if (graph_kind_ == 2) {
-      for (int i = 0; i < G / K_; ++i) enqueue_multi((graph_buf_ + i) & 1);
+    last_kind_ = e.kind;
+    if (e.kind == 2) {
+      for (int i = 0; i < G / K_; ++i) {
+        enqueue_multi(cur_);
+        issued_ += K_;
+        cur_ = nxt(cur_);
+      }
     } else {
-      for (int i = 0; i < G; ++i) enqueue_iteration((graph_parity_ + i) & 1, (graph_buf_ + i) & 1);
+      for (int i = 0; i < G; ++i) {
+        enqueue_iteration((int)(issued_ & 1), cur_);
+        ++issued_;
+        cur_ = nxt(cur_);
+      }
     }
+    flush_pending_reduce();
     ev_record(EV_JCOMM, kComm);
     ev_record(EV_JRED, kReduce);
     ev_wait(kCompute, EV_JCOMM);
     ev_wait(kCompute, EV_JRED);
     H3D_TRACE("end_capture");
-    graph_ = be_->end_capture();
     capturing_ = false;
+    e.exec = be_->end_capture();
     H3D_TRACE("graph instantiated");
-    graph_iters_ = G;
-  } catch (const std::exception& e) {
+  } catch (const std::exception& ex) {
     if (capturing_) {
+      capturing_ = false;
       try {
         be_->end_capture();
       } catch (...) {
       }
-      capturing_ = false;
     }
-    graph_ = nullptr;
+    e.exec = nullptr;
     graph_failed_ = true;
     if (!cfg_.quiet && is_root())
-      std::fprintf(stderr, "heat3d: hipGraph capture failed (%s); running eagerly\n", e.what());
+      std::fprintf(stderr, "heat3d: hipGraph capture failed (%s); running eagerly\n", ex.what());
   }
+  issued_ = s_issued;
+  nsweep_ = s_nsweep;
+  cur_ = s_cur;
+  last_kind_ = s_last;
+  pending_.valid = false;
   std::memcpy(ev_valid_, saved, sizeof(saved));
   std::memcpy(cur_ev_, saved_cur, sizeof(saved_cur));
+  if (!e.exec) return nullptr;
+  if (graphs_.size() >= 8) {
+    be_->sync_all();
+    be_->destroy_graph(graphs_.front().exec);
+    graphs_.erase(graphs_.begin());
+  }
+  graphs_.push_back(e);
+  return &graphs_.back();
+}
+
+void Solver::prepare_steps(int64_t n) {
+  if (!graphs_allowed()) return;
+  const int G = graph_len_for(n);
+  if (G > 0 && !find_graph(G)) build_graph(G);
 }
 
 void Solver::run_chunk(int64_t n) {
-  // The overlapped schedule forks the comm stream; hipStreamEndCapture of that
-  // three-stream pattern crashes on ROCm 7.0/7.2 (see docs/ARCHITECTURE.md), so
-  // graphs are used for the single-stream schedules (the launch-bound small
-  // and single-GPU cases) unless HEAT3D_GRAPH_MULTISTREAM=1.
-  static const bool ms_ok = [] {
-    const char* e = std::getenv("HEAT3D_GRAPH_MULTISTREAM");
-    return e && e[0] == '1';
-  }();
-  const bool graphs = cfg_.use_graph && be_->supports_graphs() && comm_->capturable() && nbuf_ == 2 &&
-                      !graph_failed_ && !phase_timing_ && (!multi_stream() || ms_ok);
-  const int want_kind = tb_ ? 2 : 1;
+  const bool graphs = graphs_allowed();
   while (n > 0) {
-    int G = std::max(2, cfg_.graph_chunk - (cfg_.graph_chunk & 1));
-    if (tb_) G = std::max(2 * K_, G - (G % (2 * K_)));
-    if (graph_ && graph_kind_ != want_kind) {
-      be_->sync_all();
-      be_->destroy_graph(graph_);
-      graph_ = nullptr;
-    }
-    const bool aligned = graph_ && (int)(issued_ & 1) == graph_parity_ && cur() == graph_buf_;
-    if (graphs && n >= G && (graph_ == nullptr || aligned)) {
-      if (!graph_) build_graph();
-      if (graph_ && (int)(issued_ & 1) == graph_parity_ && cur() == graph_buf_) {
-        H3D_TRACE("launch_graph issued=" << issued_);
+    const int G = graphs ? graph_len_for(n) : 0;
+    if (G > 0) {
+      GraphEntry* g = find_graph(G);
+      if (!g) g = build_graph(G);
+      if (g) {
+        H3D_TRACE("launch_graph G=" << G << " issued=" << issued_);
         // the graph is launched on the compute stream: order it after work
         // still pending on the other streams (e.g. an overlapped single step)
         join_pipeline();
-        last_kind_ = graph_kind_;
-        be_->launch_graph(graph_);
-        if (graph_kind_ == 2) {
-          for (int i = 0; i < graph_iters_ / K_; ++i) {
+        be_->launch_graph(g->exec);
+        ++graph_launches_;
+        if (g->kind == 2) {
+          for (int i = 0; i < G / K_; ++i) {
             record_segment(issued_, K_, cur());
             issued_ += K_;
             cur_ = nxt(cur_);
+            if (tb_overlap_) ++nsweep_;  // as enqueue_multi counts them
           }
         } else {
-          for (int i = 0; i < graph_iters_; ++i) {
+          for (int i = 0; i < G; ++i) {
             record_segment(issued_, 1, cur());
             ++issued_;
             cur_ = nxt(cur_);
           }
         }
-        n -= graph_iters_;
+        n -= G;
+        last_kind_ = g->kind;
         // the graph joined every stream into compute: re-fork for eager work
         for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
         ev_record(EV_FORK, kCompute);
@@ -846,6 +941,7 @@ void Solver::run_chunk(int64_t n) {
     cur_ = nxt(cur_);
     --n;
   }
+  flush_pending_reduce();
 }
 
 void Solver::step(int64_t n) { run_chunk(n); }

@@ -85,9 +85,14 @@ class Solver {
   RunResult run();
   // Enqueue exactly n iterations without host polling (benchmarks); async.
   void step(int64_t n);
+  // Capture (untimed) the hipGraph that step(n) will replay from the current
+  // state, so that a timed step(n) only launches it.  No-op when graphs are off.
+  void prepare_steps(int64_t n);
   void synchronize();
   HostState state();
   int64_t iterations_issued() const { return issued_; }
+  // hipGraph launches so far (what actually ran, not the --graph request)
+  int64_t graph_launches() const { return graph_launches_; }
 
   // Error vs analytic steady state (heat3D.cu:1093-1106, with a true global
   // mean instead of rank-0's local value).  Uses the current field.
@@ -168,6 +173,19 @@ class Solver {
   template <typename Pred>
   void enqueue_halo_phase(int bi, StreamId s, Pred in_phase);
   void join_pipeline();      // every stream waits for every pipeline event
+  // Collective ordering chain (ordered_collectives comms, > 1 rank): every
+  // exchange / all-reduce waits for the previous one's completion event, so
+  // each GPU runs the job's collectives in one total order, the host issue
+  // order, which is identical on all ranks.
+  void comm_token_wait(StreamId s);
+  void comm_token_signal(StreamId s);
+  // all-reduce + check of one sweep (residual slots slot0 .. slot0+Kp-1)
+  void reduce_and_check(StreamId s, int slot0, int Kp);
+  // lagged overlapped sweeps: the all-reduce of sweep q is issued after the
+  // halo of sweep q+1 (see enqueue_multi); flush issues a pending one
+  void flush_pending_reduce();
+  bool graphs_allowed() const;
+  int graph_len_for(int64_t n) const;
   bool multi_stream() const { return tb_ ? tb_overlap_ : overlap_; }
   // buffer holding T^{issued_}; a step or a K-step sweep reads cur() and
   // writes nxt(cur())
@@ -180,7 +198,14 @@ class Solver {
   void ev_record(int id, StreamId s);
   void ev_wait(StreamId s, int id);
   void run_chunk(int64_t n);
-  void build_graph();
+  // graph replaying G iterations from the current (buffer, parity) state
+  struct GraphEntry {
+    void* exec = nullptr;
+    int G = 0, kind = 1, buf = 0, parity = 0, sparity = 0;
+  };
+  GraphEntry* find_graph(int G);
+  GraphEntry* build_graph(int G);
+  void destroy_graphs();
   InitParams init_params(const Local& l) const;
 
   Config cfg_;
@@ -225,7 +250,12 @@ class Solver {
 
   // events: 0..1 int[p], 2..3 bnd[p], 4..5 check[p], 6 fork, 7 join comm, 8 join red, 9..10 poll
   enum { EV_INT = 0, EV_BND = 2, EV_CHK = 4, EV_FORK = 6, EV_JCOMM = 7, EV_JRED = 8, EV_POLL = 9,
-         EV_T0 = 11, EV_T1 = 12, EV_COUNT = 16 };
+         EV_T0 = 11, EV_T1 = 12, EV_TOKEN = 13, EV_COUNT = 16 };
+  bool chain_ = false;              // collective ordering chain active
+  struct PendingReduce {
+    bool valid = false;
+    int q = 0, slot0 = 0, Kp = 0;
+  } pending_;
   Event ev_[EV_COUNT] = {};
   Event cur_ev_[EV_COUNT] = {};     // event currently standing for each id
   std::vector<Event> cap_pool_;     // fresh events for records inside a capture
@@ -233,12 +263,9 @@ class Solver {
   bool ev_valid_[EV_COUNT] = {};
   bool capturing_ = false;
 
-  void* graph_ = nullptr;
-  int graph_iters_ = 0;
-  int graph_parity_ = 0;
-  int graph_buf_ = 0;     // input buffer at the start of the captured chunk
-  int graph_kind_ = 1;    // 1 = single-step iterations, 2 = temporally blocked sweeps
+  std::vector<GraphEntry> graphs_;  // small cache, keyed by (G, kind, buf, parities)
   bool graph_failed_ = false;
+  int64_t graph_launches_ = 0;
 
   bool phase_timing_ = false;
   std::vector<std::pair<std::string, double>> phase_acc_;

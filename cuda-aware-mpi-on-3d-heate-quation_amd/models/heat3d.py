@@ -169,6 +169,11 @@ class HeatSolver:
     def synchronize(self) -> None:
         self._s.synchronize()
 
+    def prepare_steps(self, n: int) -> None:
+        """Capture (untimed) the hipGraph that ``step(n)`` will replay."""
+        self._ensure()
+        self._s.prepare_steps(int(n))
+
     def state(self) -> Dict:
         return dict(self._s.state())
 

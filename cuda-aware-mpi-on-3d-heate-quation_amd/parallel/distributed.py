@@ -125,6 +125,17 @@ def barrier(group=None):
         dist.barrier(group=group)
 
 
+def all_gather_objects(obj, group=None) -> list:
+    """Host-side all-gather of a picklable object (bootstrap group); [obj] alone."""
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
 def max_over_ranks(value: float, group=None) -> float:
     """Host-side max of a scalar over ranks (gloo bootstrap group)."""
     import torch
