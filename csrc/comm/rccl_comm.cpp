@@ -124,7 +124,7 @@ class RcclComm final : public Comm {
   bool ordered_collectives() const override { return true; }
 
   void exchange(const std::vector<Transfer>& xs, Backend& be, StreamId s) override {
-    hipStream_t st = static_cast<hipStream_t>(be.stream(s));
+    hipStream_t st = static_cast<hipStream_t>(be.op_begin(s));
     NCCL_CHECK(ncclGroupStart());
     for (const auto& x : xs) {
       ncclDataType_t dt;
@@ -136,26 +136,30 @@ class RcclComm final : public Comm {
       if (x.dst_rank == rank_) NCCL_CHECK(ncclRecv(x.dst, cnt, dt, x.src_rank, halo_, st));
     }
     NCCL_CHECK(ncclGroupEnd());
+    be.op_end(s);
   }
   void allreduce(void* buf, std::size_t count, RedType t, RedOp op, Backend& be,
                  StreamId s) override {
-    hipStream_t st = static_cast<hipStream_t>(be.stream(s));
+    hipStream_t st = static_cast<hipStream_t>(be.op_begin(s));
     NCCL_CHECK(ncclAllReduce(buf, buf, count, to_nccl(t), op == RedOp::Max ? ncclMax : ncclSum,
                              red_, st));
+    be.op_end(s);
   }
   void send(const void* buf, std::size_t bytes, int peer, Backend& be, StreamId s) override {
-    hipStream_t st = static_cast<hipStream_t>(be.stream(s));
+    hipStream_t st = static_cast<hipStream_t>(be.op_begin(s));
     ncclDataType_t dt;
     std::size_t cnt;
     message_shape(bytes, &dt, &cnt);
     NCCL_CHECK(ncclSend(buf, cnt, dt, peer, halo_, st));
+    be.op_end(s);
   }
   void recv(void* buf, std::size_t bytes, int peer, Backend& be, StreamId s) override {
-    hipStream_t st = static_cast<hipStream_t>(be.stream(s));
+    hipStream_t st = static_cast<hipStream_t>(be.op_begin(s));
     ncclDataType_t dt;
     std::size_t cnt;
     message_shape(bytes, &dt, &cnt);
     NCCL_CHECK(ncclRecv(buf, cnt, dt, peer, halo_, st));
+    be.op_end(s);
   }
   void barrier(Backend& be) override {
     if (!bar_ && hipMalloc(&bar_, 8) != hipSuccess) HEAT3D_THROW("hipMalloc failed");

@@ -38,6 +38,12 @@ class Backend {
   virtual void memset(void* dst, int v, std::size_t bytes, StreamId s) = 0;
 
   virtual void* stream(StreamId s) = 0;  // native handle (hipStream_t) or nullptr
+  // Bracket work that a caller enqueues itself on stream s (RCCL calls):
+  // op_begin returns the native stream to enqueue on — the real stream, or,
+  // while a graph is being recorded, a private stream capturing this one
+  // operation — and op_end closes it.
+  virtual void* op_begin(StreamId s) { return stream(s); }
+  virtual void op_end(StreamId /*s*/) {}
   virtual Event event_create() = 0;
   virtual void event_destroy(Event e) = 0;
   virtual void record(Event e, StreamId s) = 0;
@@ -48,7 +54,11 @@ class Backend {
   virtual void sync(StreamId s) = 0;
   virtual void sync_all() = 0;
 
-  // graph capture of the compute stream (forks onto the other streams via events)
+  // Graph recording: between begin_capture and end_capture nothing runs;
+  // every operation on any stream becomes a node of one graph, and event
+  // record / wait pairs become its dependency edges (HipBackend builds the
+  // graph explicitly, see hip_backend.cpp).  The executable graph is launched
+  // on the compute stream.
   virtual bool supports_graphs() const { return false; }
   virtual void begin_capture() {}
   virtual void* end_capture() { return nullptr; }  // returns executable graph

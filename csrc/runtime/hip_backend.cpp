@@ -1,5 +1,17 @@
 // heat3d-mi355x — HIP backend: one device, three prioritised streams,
-// event pool, pinned host staging and hipGraph capture.
+// event pool, pinned host staging and explicitly built hipGraphs.
+//
+// Graphs.  Stream capture of the solver's three-stream schedule (compute,
+// comm, reduce, forking and joining through events) overflows the host stack
+// inside hipStreamEndCapture of the HIP runtime PyTorch ships (a recursion
+// through the streams' parallel-capture lists; backtrace in
+// docs/ARCHITECTURE.md, minimal single-op patterns in
+// tools/graph_capture_repro.hip do not trigger it).  So the graph is built
+// explicitly: while recording, each operation is captured alone on a private
+// stream (a one-stream capture) into a child graph, added as a node that
+// depends on its stream's current frontier; an event record remembers the
+// recording stream's frontier and a wait merges it into the waiting stream's.
+// The resulting DAG has exactly the dependencies of the eager schedule.
 //
 // The device is bound once (the reference called cudaSetDevice(rank % n) in
 // every iteration, heat3D.cu:650-654).  The comm and reduce streams get the
@@ -8,8 +20,11 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
+#include <vector>
 
 #include "backend.hpp"
 
@@ -60,9 +75,12 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kCompute], hipStreamNonBlocking, least));
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kComm], hipStreamNonBlocking, greatest));
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kReduce], hipStreamNonBlocking, greatest));
+    HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
   }
   ~HipBackend() override {
     (void)hipSetDevice(dev_);
+    if (rec_) (void)hipGraphDestroy(rec_);
+    if (cap_) (void)hipStreamDestroy(cap_);
     if (err_scratch_) (void)hipFree(err_scratch_);
     for (auto& s : streams_)
       if (s) (void)hipStreamDestroy(s);
@@ -96,13 +114,38 @@ class HipBackend final : public Backend {
       case CopyKind::D2D: kind = hipMemcpyDeviceToDevice; break;
       case CopyKind::H2H: kind = hipMemcpyHostToHost; break;
     }
-    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, kind, streams_[s]));
+    op(s, [&](hipStream_t st) { HIP_CHECK(hipMemcpyAsync(dst, src, bytes, kind, st)); });
   }
   void memset(void* dst, int v, std::size_t bytes, StreamId s) override {
-    HIP_CHECK(hipMemsetAsync(dst, v, bytes, streams_[s]));
+    op(s, [&](hipStream_t st) { HIP_CHECK(hipMemsetAsync(dst, v, bytes, st)); });
   }
 
   void* stream(StreamId s) override { return streams_[s]; }
+  void* op_begin(StreamId s) override {
+    if (!recording_) return streams_[s];
+    HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
+    in_op_ = true;
+    op_s_ = s;
+    HIP_CHECK(hipStreamBeginCapture(cap_, hipStreamCaptureModeThreadLocal));
+    return cap_;
+  }
+  void op_end(StreamId s) override {
+    if (!recording_) return;
+    HEAT3D_CHECK(in_op_ && op_s_ == s, "graph recording: unbalanced operation");
+    in_op_ = false;
+    hipGraph_t g = nullptr;
+    HIP_CHECK(hipStreamEndCapture(cap_, &g));
+    std::size_t n = 0;
+    hipError_t e = hipGraphGetNodes(g, nullptr, &n);
+    if (e == hipSuccess && n > 0) {
+      hipGraphNode_t node = nullptr;
+      auto& t = tail_[s];
+      e = hipGraphAddChildGraphNode(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), g);
+      if (e == hipSuccess) t.assign(1, node);
+    }
+    (void)hipGraphDestroy(g);
+    HIP_CHECK(e);
+  }
   Event event_create() override {
     hipEvent_t e;
     HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDefault));
@@ -110,9 +153,23 @@ class HipBackend final : public Backend {
   }
   void event_destroy(Event e) override { (void)hipEventDestroy(static_cast<hipEvent_t>(e)); }
   void record(Event e, StreamId s) override {
+    if (recording_) {
+      evn_[e] = tail_[s];  // the recording stream's frontier
+      return;
+    }
     HIP_CHECK(hipEventRecord(static_cast<hipEvent_t>(e), streams_[s]));
   }
   void wait(StreamId s, Event e) override {
+    if (recording_) {
+      // an event recorded before the recording started is already complete
+      // when the graph (launched behind a join of every stream) runs
+      auto it = evn_.find(e);
+      if (it == evn_.end()) return;
+      auto& t = tail_[s];
+      for (hipGraphNode_t n : it->second)
+        if (std::find(t.begin(), t.end(), n) == t.end()) t.push_back(n);
+      return;
+    }
     HIP_CHECK(hipStreamWaitEvent(streams_[s], static_cast<hipEvent_t>(e), 0));
   }
   bool query(Event e) override {
@@ -135,14 +192,29 @@ class HipBackend final : public Backend {
 
   bool supports_graphs() const override { return true; }
   void begin_capture() override {
-    HIP_CHECK(hipStreamBeginCapture(streams_[kCompute], hipStreamCaptureModeRelaxed));
+    HEAT3D_CHECK(!recording_, "graph recording already active");
+    HIP_CHECK(hipGraphCreate(&rec_, 0));
+    for (auto& t : tail_) t.clear();
+    evn_.clear();
+    in_op_ = false;
+    recording_ = true;
   }
   void* end_capture() override {
-    hipGraph_t g = nullptr;
-    HIP_CHECK(hipStreamEndCapture(streams_[kCompute], &g));
+    HEAT3D_CHECK(recording_, "no graph recording active");
+    recording_ = false;
+    if (in_op_) {  // an operation threw while being captured
+      in_op_ = false;
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(cap_, &g);
+      if (g) (void)hipGraphDestroy(g);
+    }
+    hipGraph_t g = rec_;
+    rec_ = nullptr;
+    evn_.clear();
     hipGraphExec_t ex = nullptr;
-    HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-    HIP_CHECK(hipGraphDestroy(g));
+    hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIP_CHECK(e);
     return ex;
   }
   void launch_graph(void* ex) override {
@@ -153,40 +225,40 @@ class HipBackend final : public Backend {
   }
 
   void init_field(DType t, const InitParams& p, StreamId s) override {
-    hip::init_field(t, p, streams_[s]);
+    op(s, [&](hipStream_t st) { hip::init_field(t, p, st); });
   }
   void stencil(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) override {
-    hip::stencil(t, p, k, streams_[s]);
+    op(s, [&](hipStream_t st) { hip::stencil(t, p, k, st); });
   }
   void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) override {
-    hip::sweep(t, p, k, streams_[s]);
+    op(s, [&](hipStream_t st) { hip::sweep(t, p, k, st); });
   }
   void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, StreamId s) override {
-    hip::pack_box(t, f, L, b, buf, streams_[s]);
+    op(s, [&](hipStream_t st) { hip::pack_box(t, f, L, b, buf, st); });
   }
   void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, StreamId s) override {
-    hip::unpack_box(t, f, L, b, buf, streams_[s]);
+    op(s, [&](hipStream_t st) { hip::unpack_box(t, f, L, b, buf, st); });
   }
   void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
                 const Layout& Ld, const Box& bd, StreamId s) override {
-    hip::copy_box(t, src, Ls, bs, dst, Ld, bd, streams_[s]);
+    op(s, [&](hipStream_t st) { hip::copy_box(t, src, Ls, bs, dst, Ld, bd, st); });
   }
-  void delay(double us, StreamId s, int blocks) override { hip::delay(us, streams_[s], blocks); }
+  void delay(double us, StreamId s, int blocks) override { op(s, [&](hipStream_t st) { hip::delay(us, st, blocks); }); }
   void check_convergence(DeviceState* st, int slot, StreamId s, int count) override {
-    hip::check_convergence(st, slot, streams_[s], count);
+    op(s, [&](hipStream_t q) { hip::check_convergence(st, slot, q, count); });
   }
   void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
                         const int64_t gstart[3], double hy, DeviceState* st, StreamId s) override {
     if (!err_scratch_) err_scratch_ = static_cast<double*>(alloc(sizeof(double) * hip::error_scratch_elems()));
-    hip::error_accumulate(t, f, L, box, gstart, hy, err_scratch_, st, streams_[s]);
+    op(s, [&](hipStream_t q) { hip::error_accumulate(t, f, L, box, gstart, hy, err_scratch_, st, q); });
   }
   void poke(DType t, void* f, const Layout& L, int64_t i, int64_t j, int64_t k, double value,
             StreamId s) override {
-    hip::poke(t, f, L, i, j, k, value, streams_[s]);
+    op(s, [&](hipStream_t st) { hip::poke(t, f, L, i, j, k, value, st); });
   }
   void box_bitsum(DType t, const void* f, const Layout& L, const Box& b, unsigned long long* out,
                   StreamId s) override {
-    hip::box_bitsum(t, f, L, b, out, streams_[s]);
+    op(s, [&](hipStream_t st) { hip::box_bitsum(t, f, L, b, out, st); });
   }
   void range_push(const char* n) override {
     if (roctx_.push) roctx_.push(n);
@@ -196,8 +268,35 @@ class HipBackend final : public Backend {
   }
 
  private:
+  // run one operation: directly on the stream, or recorded as a graph node
+  template <typename F>
+  void op(StreamId s, F&& f) {
+    hipStream_t st = static_cast<hipStream_t>(op_begin(s));
+    if (!recording_) {
+      f(st);
+      return;
+    }
+    try {
+      f(st);
+    } catch (...) {
+      in_op_ = false;
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(cap_, &g);
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    op_end(s);
+  }
+
   int dev_;
   hipStream_t streams_[kNumStreams] = {nullptr, nullptr, nullptr};
+  // graph recording state
+  bool recording_ = false, in_op_ = false;
+  StreamId op_s_ = kCompute;
+  hipGraph_t rec_ = nullptr;
+  hipStream_t cap_ = nullptr;                        // private one-operation capture stream
+  std::vector<hipGraphNode_t> tail_[kNumStreams];    // dependency frontier per stream
+  std::unordered_map<Event, std::vector<hipGraphNode_t>> evn_;  // event -> frontier at record
   double* err_scratch_ = nullptr;
   Roctx roctx_;
 };

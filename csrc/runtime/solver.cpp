@@ -11,10 +11,45 @@
 #include <sstream>
 #include <thread>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include "../comm/net.hpp"
 #include "../io/io.hpp"
 
 namespace heat3d {
+
+// HEAT3D_SEGV_TRACE=1: (re-)install a fatal-signal handler printing the
+// native backtrace right before a graph capture (the HIP / torch runtimes
+// install their own handlers after the Python extension's).
+static void segv_trace_handler(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "\nheat3d: fatal signal, native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+static void arm_segv_trace() {
+  const char* e = std::getenv("HEAT3D_SEGV_TRACE");
+  if (!e || !*e || e[0] == '0') return;
+  // an alternate signal stack, so that a stack overflow is reported too
+  static char* alt = nullptr;
+  if (!alt) {
+    alt = new char[1 << 16];
+    stack_t ss{};
+    ss.ss_sp = alt;
+    ss.ss_size = 1 << 16;
+    sigaltstack(&ss, nullptr);
+  }
+  struct sigaction sa {};
+  sa.sa_handler = segv_trace_handler;
+  sa.sa_flags = SA_ONSTACK;
+  sigemptyset(&sa.sa_mask);
+  for (int s : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT}) sigaction(s, &sa, nullptr);
+}
 
 // ---------------------------------------------------------------------------
 // KernelSpec
@@ -769,11 +804,12 @@ int Solver::graph_len_for(int64_t n) const {
 }
 
 bool Solver::graphs_allowed() const {
-  // Multi-stream (overlapped) schedules: HEAT3D_GRAPH_MULTISTREAM=1 (capture of
-  // the three-stream fork/join crashes in the HIP runtime, docs/ARCHITECTURE.md)
+  // Multi-stream (overlapped) schedules are graphs too (built explicitly by
+  // the backend's recorder); HEAT3D_GRAPH_MULTISTREAM=0 restricts graphs to
+  // the single-stream schedules.
   static const bool ms_ok = [] {
     const char* e = std::getenv("HEAT3D_GRAPH_MULTISTREAM");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return cfg_.use_graph && be_->supports_graphs() && comm_->capturable() && !graph_failed_ && !phase_timing_ &&
          (!multi_stream() || ms_ok);
@@ -818,6 +854,7 @@ Solver::GraphEntry* Solver::build_graph(int G) {
   const std::size_t need = 16 * (std::size_t)G + 16;
   while (cap_pool_.size() < need) cap_pool_.push_back(be_->event_create());
   cap_next_ = 0;
+  arm_segv_trace();
   try {
     be_->begin_capture();
     capturing_ = true;
@@ -852,7 +889,7 @@ Solver::GraphEntry* Solver::build_graph(int G) {
     if (capturing_) {
       capturing_ = false;
       try {
-        be_->end_capture();
+        be_->destroy_graph(be_->end_capture());
       } catch (...) {
       }
     }
