@@ -112,3 +112,33 @@ def native_staged_cpu_worker(rank, world, port, outdir, n, eps, decomp, extra_ar
             f.write(f"{r['conv_iter']}\n")
     dist.barrier()
     dist.destroy_process_group()
+
+
+def native_rccl_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, extra_args=(), env=None):
+    """Native engine, HIP backend, a real multi-rank RCCL communicator with all
+    ranks on the one visible GPU: every rank gets its own NCCL_HOSTID, so RCCL
+    accepts the shared device (it refuses two ranks per GPU of one host) and
+    carries the traffic over its network transport on loopback.  Exercises
+    RcclComm::exchange (ncclSend / ncclRecv groups with real peers) and the
+    all-reduce of the residual slots through the production schedule."""
+    os.environ.update({"NCCL_HOSTID": f"heat3d-test-rank{rank}", "NCCL_SOCKET_IFNAME": "lo"})
+    if env:
+        os.environ.update(env)
+    dist = _init(rank, world, port)
+    import heat3d_amd
+
+    s = heat3d_amd.HeatSolver((n, n, n), 10 ** 6, eps, backend="hip", comm="rccl", decomp=decomp,
+                              dtype=dtype, device=0, extra_args=list(extra_args))
+    assert s.native.comm_name.startswith("rccl"), s.native.comm_name
+    assert s.native.comm_transport_ranks == world
+    r = s.run()
+    assert s.native.verify_halos() == 0  # checksums exchanged over RCCL
+    g = s.gather()  # ncclSend / ncclRecv of every rank's block to rank 0
+    if rank == 0:
+        np.save(os.path.join(outdir, "field.npy"), g)
+        with open(os.path.join(outdir, "result.txt"), "w") as f:
+            f.write(f"{r['conv_iter']} {r['error_percent']!r} {s.native.comm_name} {s.native.graph_launches}\n")
+    else:
+        assert g is None
+    dist.barrier()
+    dist.destroy_process_group()

@@ -1,0 +1,87 @@
+"""RCCL on the one-GPU box (SURVEY.md §5 "Distributed communication backend").
+
+* ``rccl_self_exchange``: RcclComm::exchange / allreduce on a one-rank
+  communicator — ncclSend / ncclRecv to self inside one group, byte counts
+  that are and are not multiples of 8, a padded K-deep x halo plane moved in
+  place between two ghosted fields (the solver's x-face message), all-reduce
+  identities.
+* Real multi-rank RCCL: 2 and 4 processes on the one GPU, each with its own
+  NCCL_HOSTID (RCCL refuses two ranks per device of one host; as separate
+  "hosts" its traffic takes the network transport over loopback).  The halo
+  exchange, the all-reduce of the residual slots, the halo checksums and the
+  gather all run through RcclComm with real peers; the gathered field must be
+  bitwise equal to the single-process solve, the iteration count identical.
+  Reference: heat3D.cu:619-641, 724-755 (halo), 1062-1063 (reduction),
+  1112-1162 (gather).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT, free_port
+from _mp_workers import native_rccl_gpu_worker
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rccl_self_exchange(ext, gpu):
+    r = ext.rccl_self_exchange(0, [8, 24, 1000, 4093, 1 << 20, 3 * (1 << 20) + 5], (6, 7, 9), 3)
+    assert all(r["ok"]), r
+    assert r["touched_outside"] == 0
+    assert r["transport_ranks"] == 1
+    assert r["allreduce_u64"] == (7, 0x7FF0000000000000, 3)
+    assert r["allreduce_f64"] == (1.5, -2.25)
+
+
+@pytest.mark.parametrize("world,decomp,env", [
+    (2, (2, 1, 1), None),
+    (2, (2, 1, 1), {"HEAT3D_RCCL_SHARED": "1"}),     # one communicator for halos and all-reduce
+    (4, (2, 2, 1), None),                             # block: deep y halos, axis-ordered phases
+])
+def test_rccl_multirank_bitwise(h3d, gpu, tmp_path, world, decomp, env):
+    n, eps = 33, 1e-4
+    mp.start_processes(native_rccl_gpu_worker,
+                       args=(world, free_port(), str(tmp_path), n, eps, decomp, "fp64", [], env),
+                       nprocs=world, join=True, start_method="spawn")
+    single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="hip", device=0)
+    r1 = single.run()
+    it, err, name, graphs = open(tmp_path / "result.txt").read().split()
+    assert int(it) == r1["conv_iter"]  # the same stopping iteration as one rank
+    assert name == ("rccl(shared)" if env else "rccl")
+    assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
+
+
+def test_bench_self_launch_rccl(gpu, tmp_path):
+    """``bench.py --gpus 2`` without torchrun: the launcher starts two workers,
+    RCCL spans both (comm_ranks from ncclCommCount), halos verified before timing."""
+    out = tmp_path / "b.json"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "rccl",
+                        "--rccl-host-split", "--grid", "96", "--steps", "6", "--warmup", "3",
+                        "--converge-eps", "0", "--timeout", "100", "--json-out", str(out)],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT,
+                       env={k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")})
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    j = json.loads(lines[0])
+    assert j == json.loads(out.read_text())
+    assert j["n_gpus"] == 2 and j["comm_ranks"] == 2 and j["halo_verified"]
+    assert j["config"]["comm"] == "rccl" and j["config"]["parallelism"] == "slab 2x1x1"
+    assert j["value"] > 0 and j["steps"] == 6 and [q["rank"] for q in j["placement"]] == [0, 1]
+
+
+def test_bench_self_launch_socket(gpu, tmp_path):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "socket",
+                        "--grid", "128", "--steps", "6", "--warmup", "3", "--converge-eps", "0",
+                        "--timeout", "100"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT,
+                       env={k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")})
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert j["n_gpus"] == 2 and j["comm_ranks"] == 2 and j["config"]["comm"] == "staged-socket"
+    assert j["metric"].endswith("128^3 fp64 grid") and j["config"]["model"].endswith("128^3 fp64 grid")
