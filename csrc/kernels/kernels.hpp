@@ -20,7 +20,8 @@ struct KernelSpec {
   // TB2 / TBK / TBR advance K time steps per HBM sweep: TB2 is the tuned K = 2
   // kernel (stencil_tb2.hip), TBK the queue kernel (stencil_tbk.hip), TBR the
   // register-ring kernel (stencil_tbr.hip; its 7th field is the T^n ring size)
-  enum Kind { Naive = 0, Column = 1, Tile = 2, TB2 = 3, TBK = 4, TBR = 5 } kind = Tile;
+  // TBL: the lean K-step kernel (stencil_tbl.hip), halos as lanes / rows
+  enum Kind { Naive = 0, Column = 1, Tile = 2, TB2 = 3, TBK = 4, TBR = 5, TBL = 6 } kind = Tile;
   int K = 0;  // multi-step kinds: time steps per sweep
   int WZ = 0, WY = 0;  // tile kernel: waves per workgroup along z and y
   int V = 0;  // elements per lane along z (0 = default for dtype)
@@ -28,7 +29,7 @@ struct KernelSpec {
   int L = 0;  // x-segment length per wave (0 = auto)
   int O = -1; // tile order: 1 = z tiles fastest (default), 0 = y tiles fastest
   int NT = 0; // non-temporal output stores
-  bool multi_step() const { return kind == TB2 || kind == TBK || kind == TBR; }
+  bool multi_step() const { return kind == TB2 || kind == TBK || kind == TBR || kind == TBL; }
   static KernelSpec parse(const std::string& s);
   std::string str() const;
   // zero (default) fields replaced by the tuned defaults for dtype t
@@ -83,7 +84,9 @@ void stencil2(DType t, const StencilParams& p, const KernelSpec& k, void* stream
 void stencil_multi(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 // Same sweep, register-ring kernel (stencil_tbr.hip)
 void stencil_ring(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
-// Any multi-step kind (TB2 / TBK / TBR) -> its kernel
+// Same sweep, lean kernel (stencil_tbl.hip)
+void stencil_lean(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+// Any multi-step kind (TB2 / TBK / TBR / TBL) -> its kernel
 void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, void* stream);
 void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, void* stream);

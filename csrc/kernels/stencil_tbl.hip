@@ -1,0 +1,431 @@
+// heat3d-mi355x — K-step temporally blocked FTCS kernel, lean form ("tl").
+//
+// Same contract as stencil_tbr.hip (one HBM sweep turns T^n into T^{n+K};
+// every point goes through the reference update heat3D.cu:128-131 with the
+// arithmetic of kernels.hpp ftcs_update, so fields and all K residuals are
+// bitwise identical to K single steps), re-planned after the ISA and
+// counters of the ring kernel on MI355X: ~40% of its VALU stream per point
+// update was overhead (SGPR spill reloads through v_readlane, read-lanes of
+// separately loaded halo columns, per-point validity selects), which is what
+// kept a 4-step variant from fitting 16 waves x 128 VGPRs.  Here
+//
+//   * halos are ordinary lanes and rows: a tile loads 64 consecutive columns
+//     (one wave wide) and WY*R rows; stage s output is valid on lanes
+//     [s+1, 63-s) and tile rows [s+1, TY-s-1); T^{n+K} is stored on
+//     lanes [K, 64-K) x rows [K, TY-K).  z neighbours are zero-filling DPP
+//     shifts (no "old" operand, no read-lanes, no halo registers); the tile's
+//     outer rows take a wave's own edge row from LDS as a stand-in (finite,
+//     outside every stored / counted point);
+//   * residuals accumulate per lane without masks; the per-lane validity of
+//     stage s (cone, update range, box widened by K-1-s) is applied once, at
+//     the end;
+//   * a wave whose rows are inside the box, the update range and the tile's
+//     cone runs a mask-free step ("fast"): 9 fp64 ops for the update, 2 for
+//     the residual, 4 DPP moves.  Steps of the pipeline fill / drain, tiles on
+//     a Dirichlet face and waves on the tile's edge run the masked step (the
+//     same code with uniform x / y conditions and a per-lane z mask); the
+//     choice is a uniform branch per step, both forms hold one barrier;
+//   * loads are an SGPR row base plus one lane offset (global_load saddr
+//     form), clamped rows / planes fold into the SGPR base.
+//
+// Tiles advance along z by 64 - 2K columns and along y by WY*R - 2K rows;
+// workgroups march along x segments (XPlan, as the ring kernel), dispatched
+// XCD-aware.  y rows of each stage's centre plane go through LDS once per
+// step (double-buffered by step parity: one barrier per step).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+
+#include "hip_helpers.hpp"
+
+namespace heat3d {
+namespace hip {
+
+struct TBLArgs {
+  int64_t sx, sy, origin;      // plane / row strides, element index of owned (0,0,0)
+  int blo[3], bhi[3];          // store box
+  int ulo, uhi, uylo, uyhi;    // update ranges (x, y)
+  int uzlo, uzhi;              // update range (z)
+  int xlo_live, xhi_live;      // x planes present in memory
+  int ylo_live, yhi_live;      // y rows present in memory
+  int c00, r00;                // first loaded column / row of tile (0, 0)
+  int nzb, nyb;
+  int segsplit, n1, rb;        // x plan (TBRArgs encoding)
+};
+
+namespace {
+
+constexpr int gcd_l(int a, int b) { return b == 0 ? a : gcd_l(b, a % b); }
+constexpr int lcm_l(int a, int b) { return a / gcd_l(a, b) * b; }
+
+__device__ __forceinline__ int sgpr(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Raw buffer resource over one x plane (SGPRs: 48-bit base, no range limit;
+// dword 3 = the gfx9 untyped-buffer word).  A row load / store is then
+// buffer_{load,store}_dwordx2 v, v_lane_bytes, s[rsrc], s_row_bytes offen:
+// no per-lane 64-bit address registers, no address VALU.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)0xffffffff, 0x00020000);
+}
+template <typename Real>
+__device__ __forceinline__ Real buf_load(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  if constexpr (sizeof(Real) == 8)
+    return __builtin_bit_cast(Real, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  else
+    return __builtin_bit_cast(Real, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+template <typename Real>
+__device__ __forceinline__ void buf_store(Real v, __amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  if constexpr (sizeof(Real) == 8)
+    __builtin_amdgcn_raw_buffer_store_b64(
+        __builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), v), r, voff, soff, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+}
+
+// f(integral_constant<int, I>) for I = B .. E-1, unrolled at compile time
+template <int B, int E, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  if constexpr (B < E) {
+    fn(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(fn);
+  }
+}
+
+}  // namespace
+
+template <typename Real, int R, int WY, int K, int Q>
+__global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ in, Real* __restrict__ out,
+                                                       TBLArgs g, Real Dx, Real Dy, Real Dz,
+                                                       unsigned long long* res, const int* done) {
+  static_assert(K >= 2 && K <= 6, "temporal depth");
+  // T^n ring: Q = 3 loads plane x+2 into the slot stage 0 frees at step x
+  // ((K-1)/K of a step of latency cover); Q >= 4 loads plane x+Q-2 at the
+  // start of step x (Q-3 steps of cover)
+  static_assert(Q == 3 || Q == 4 || Q == 6, "T^n ring size");
+  constexpr int TY = WY * R;
+  constexpr int ZS = 64 - 2 * K;   // tile stride along z (stored columns)
+  constexpr int YS = TY - 2 * K;   // tile stride along y (stored rows)
+  // x-loop unroll making every ring index and the LDS parity static
+  constexpr int U = lcm_l(lcm_l(Q, 3), 2);
+  static_assert(YS > 0 && R <= 16, "tile too small for depth K");
+  __shared__ __attribute__((aligned(16))) Real s_row[2][K][WY][2][64];
+  static_assert(sizeof(s_row) >= WY * K * sizeof(unsigned long long), "residual scratch");
+  if (flag_set(done)) return;
+
+  // piece decode: blocks dealt round-robin over the 8 XCDs; consecutive
+  // pieces (neighbouring tiles) share an XCD's L2 (same encoding as tbr)
+  auto remap = [](int i, int n) {
+    const int c = i & 7;
+    return c * (n >> 3) + min(c, n & 7) + (i >> 3);
+  };
+  const int blk = blockIdx.x;
+  int pc, part;
+  const int rr = g.rb & 0x3fffffff;
+  if (blk < g.n1) {
+    pc = remap(blk, g.n1);
+    part = 0;
+  } else if (blk < g.n1 + rr) {
+    pc = g.n1 + remap(blk - g.n1, rr);
+    part = 1;
+  } else {
+    pc = g.n1 + remap(blk - g.n1 - rr, rr);
+    part = 2;
+  }
+  const int zb = pc % g.nzb;
+  const int tq = pc / g.nzb;
+  const int ybk = tq % g.nyb;
+  const int xs = tq / g.nyb;
+  const int nxb = g.bhi[0] - g.blo[0];
+  const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
+  int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
+  if (part == 1 && (g.rb >> 30)) xhi_p = min(xhi_p, xlo_p + split);
+  if (part == 2) xlo_p = min(xlo_p + split, xhi_p);
+
+  const int wave = sgpr(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int c0 = g.c00 + zb * ZS;           // tile's first loaded column
+  const int r0 = g.r00 + ybk * YS;          // tile's first loaded row
+  const int yb = r0 + wave * R;             // this wave's first row
+  const int col = c0 + lane;
+  const int xa = g.blo[0] + xlo_p, xe = g.blo[0] + xhi_p;
+  const int x0 = xa - (K - 1), xlast = xe + K - 2;
+  const int64_t sx = g.sx;
+
+  // ---- uniform (per wave) classification
+  const bool zfast = c0 >= g.uzlo && c0 + 64 <= g.uzhi;
+  const bool wrows = wave * R >= K && wave * R + R <= TY - K && yb >= g.uylo && yb + R <= g.uyhi &&
+                     yb >= g.blo[1] && yb + R <= g.bhi[1];
+  const bool wfast = zfast && wrows;
+  // steps whose every stage is valid, updated, counted and (last stage) stored
+  const int xf_lo = max(max(x0 + 2 * (K - 1), g.ulo + K - 1), g.blo[0] + K - 1);
+  const int xf_hi = min(min(xlast, g.uhi - 1), g.bhi[0] + K - 2);
+
+  // masked form, per row r (uniform, one SGPR): bit r = row in the update
+  // range, bit R + r = stored row, bit 2R + s*R + r = row counted at stage s
+  unsigned ybits = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int row = yb + r, rp = wave * R + r;
+    if (row >= g.uylo && row < g.uyhi) ybits |= 1u << r;
+    if (rp >= K && rp < TY - K && row >= g.blo[1] && row < g.bhi[1]) ybits |= 1u << (R + r);
+#pragma unroll
+    for (int s = 0; s < K; ++s)
+      if (row >= g.uylo && row < g.uyhi && rp >= s + 1 && rp < TY - s - 1 && row >= g.blo[1] - (K - 1 - s) &&
+          row < g.bhi[1] + (K - 1 - s))
+        ybits |= 1u << (2 * R + s * R + r);
+  }
+  ybits = (unsigned)sgpr((int)ybits);
+  static_assert(2 * R + K * R <= 32, "row mask bits");
+
+  // per-lane masks (constant over the sweep)
+  const bool zin = col >= g.uzlo && col < g.uzhi;
+  const bool zst = lane >= K && lane < 64 - K && col >= g.blo[2] && col < g.bhi[2];
+
+  // ---- addressing: uniform base of row yb, column c0; clamped row offsets
+  // (uniform by construction: kernel arguments and the readfirstlane'd wave
+  // index; pointers stay in the global address space)
+  // Loads: base at the wave's first clamped row; a buffer soffset is an
+  // unsigned 32-bit value, so every row offset must be >= 0 (clamping is
+  // monotonic: clamp(yb + r) >= clamp(yb)).  Stores only touch stored rows,
+  // which are real rows at or after yb.
+  auto yclamp = [&](int row) { return min(max(row, g.ylo_live), g.yhi_live); };
+  const int ybc = yclamp(yb);
+  const Real* __restrict__ inw = in + (g.origin + (int64_t)ybc * g.sy + c0);
+  Real* __restrict__ outw = out + (g.origin + (int64_t)yb * g.sy + c0);
+  // row byte offsets (clamped rows fold in), 0 <= roff < 2^31: checked in launch_tbl
+  int roff[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) roff[r] = sgpr((yclamp(yb + r) - ybc) * (int)g.sy * (int)sizeof(Real));
+  const int sy_b = (int)g.sy * (int)sizeof(Real);
+  const unsigned lane_b = (unsigned)lane * (unsigned)sizeof(Real);
+
+  Real q[Q][R];              // T^n ring: plane p in slot (p - x0 + 1) mod Q
+  Real f[K - 1][3][R];       // F_{s+1}(p) in f[s][(p + s) mod 3]
+  double m[K];               // per-lane residual maxima
+  bool nan_seen = false;
+#pragma unroll
+  for (int s = 0; s < K; ++s) m[s] = 0.0;
+#pragma unroll
+  for (int s = 0; s < K - 1; ++s)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int r = 0; r < R; ++r) f[s][i][r] = Real(0);
+
+  auto load_plane = [&](int x, Real (&d)[R]) {
+    const int xc = min(max(x, g.xlo_live), g.xhi_live);
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(inw + (int64_t)xc * sx);
+#pragma unroll
+    for (int r = 0; r < R; ++r) d[r] = buf_load<Real>(rs, lane_b, roff[r]);
+  };
+  constexpr int NPRE = Q == 3 ? 3 : Q - 1;  // planes resident / in flight before step x0
+#pragma unroll
+  for (int i = 0; i < NPRE; ++i) load_plane(x0 - 1 + i, q[i]);
+
+  // One plane step.  FAST: every condition below is known true.
+  auto step = [&](auto fast_tag, const int x, auto ph_tag) {
+    constexpr bool FAST = decltype(fast_tag)::value;
+    constexpr int ph = decltype(ph_tag)::value;
+    constexpr int sM = ph % Q, sC = (ph + 1) % Q, sP = (ph + 2) % Q;
+    constexpr int fw = ph % 3, fc = (ph + 2) % 3, fm = (ph + 1) % 3;
+    constexpr int par = ph & 1;  // LDS buffer (U is even)
+    if constexpr (Q >= 4) load_plane(x + Q - 2, q[(ph + Q - 1) % Q]);
+    // publish the edge rows of every stage's centre plane
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      const Real(&C)[R] = s == 0 ? q[sC] : f[s > 0 ? s - 1 : 0][fc];
+      s_row[par][s][wave][0][lane] = C[0];
+      s_row[par][s][wave][1][lane] = C[R - 1];
+    }
+    __syncthreads();
+    const int wl = max(wave - 1, 0), wh = min(wave + 1, WY - 1);
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      Real(&M)[R] = s == 0 ? q[sM] : f[s > 0 ? s - 1 : 0][fm];
+      Real(&C)[R] = s == 0 ? q[sC] : f[s > 0 ? s - 1 : 0][fc];
+      Real(&P)[R] = s == 0 ? q[sP] : f[s > 0 ? s - 1 : 0][fw];
+      const Real lo = s_row[par][s][wl][1][lane];
+      const Real hi = s_row[par][s][wh][0][lane];
+      const int p = x - s;
+      // masked form: uniform x conditions of this stage
+      bool xin = true, xcnt = true, xst = true;
+      if constexpr (!FAST) {
+        xin = p >= g.ulo && p < g.uhi;
+        xcnt = xin && x >= x0 + 2 * s && x <= xlast && p >= g.blo[0] - (K - 1 - s) && p < g.bhi[0] + (K - 1 - s);
+        xst = p >= xa && p < xe;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const Real ym = r == 0 ? lo : C[r > 0 ? r - 1 : 0];
+        const Real yp = r == R - 1 ? hi : C[r + 1 < R ? r + 1 : 0];
+        const Real zm = dpp_shr1z(C[r]);
+        const Real zp = dpp_shl1z(C[r]);
+        const Real nv = ftcs<Real>(C[r], M[r], P[r], ym, yp, zm, zp, Dx, Dy, Dz);
+        const double d = fabs((double)nv - (double)C[r]);
+        bool upd = true, cnt = true, st = true;
+        if constexpr (!FAST) {
+          upd = xin && ((ybits >> r) & 1u);
+          cnt = xcnt && ((ybits >> (2 * R + s * R + r)) & 1u);
+          st = xst && ((ybits >> (R + r)) & 1u);
+        }
+        if (s < K - 1) {
+          Real(&N)[R] = f[s < K - 1 ? s : 0][fw];
+          if constexpr (FAST) N[r] = nv;
+          else N[r] = (upd && zin) ? nv : C[r];
+        }
+        if constexpr (FAST) {
+          m[s] = fmax(m[s], d);
+        } else {
+          if (cnt) m[s] = fmax(m[s], d);
+        }
+        if (s == K - 1 && st) {
+          // T^{n+K} on the stored region (inside the box, hence the update range)
+          nan_seen |= zst && (nv != nv);
+          if (zst) buf_store<Real>(nv, plane_rsrc(outw + (int64_t)p * sx), lane_b, r * sy_b);
+        }
+      }
+      if constexpr (Q == 3) {
+        if (s == 0) load_plane(x + 2, q[sM]);  // the slot stage 0 has just freed
+      }
+    }
+  };
+
+  // whole chunks of U steps (the unrolled body needs a constant trip count);
+  // padded steps past xlast take the masked form and count / store nothing
+  for (int xb = x0; xb <= xlast; xb += U) {
+    static_for<0, U>([&](auto ph_tag) {
+      constexpr int ph = decltype(ph_tag)::value;
+      const int x = xb + ph;
+      if (wfast && x >= xf_lo && x <= xf_hi) step(std::true_type{}, x, ph_tag);
+      else step(std::false_type{}, x, ph_tag);
+    });
+  }
+
+  if (res) {
+    double mm[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      // stage s counts lanes inside its cone, the update range and the box
+      // widened by K-1-s (deep-halo points still in flight stay excluded)
+      const bool ok = zin && lane >= s + 1 && lane < 63 - s && col >= g.blo[2] - (K - 1 - s) &&
+                      col < g.bhi[2] + (K - 1 - s);
+      mm[s] = ok ? m[s] : 0.0;
+    }
+    // the row exchange buffer is dead: reuse it for the per-wave maxima
+    __syncthreads();
+    residual_commit_block<WY, K>(res, mm, nan_seen,
+                                 *reinterpret_cast<unsigned long long(*)[WY][K]>(&s_row[0][0][0][0][0]));
+  }
+}
+
+template <typename Real, int R, int WY, int K, int Q>
+static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
+  const Box& b = p.box;
+  constexpr int TY = WY * R;
+  const Layout& L = p.L;
+  HEAT3D_CHECK(L.n[0] + 2 * L.gx < (1LL << 30) && L.n[1] + 2 * L.gy < (1LL << 30) &&
+                   L.sy * (int64_t)sizeof(Real) * (R + 2 * L.gy + TY + 2 * K) < (1LL << 31),
+               "tl: extents exceed 32-bit tile coordinates");
+  TBLArgs g;
+  g.sx = L.sx;
+  g.sy = L.sy;
+  g.origin = L.origin;
+  for (int a = 0; a < 3; ++a) {
+    g.blo[a] = (int)b.lo[a];
+    g.bhi[a] = (int)b.hi[a];
+  }
+  g.ulo = (int)(p.ux[1] >= p.ux[0] ? p.ux[0] : b.lo[0]);
+  g.uhi = (int)(p.ux[1] >= p.ux[0] ? p.ux[1] : b.hi[0]);
+  const bool wy = p.uy[1] >= p.uy[0], wz = p.uz[1] >= p.uz[0];
+  g.uylo = (int)(wy ? p.uy[0] : b.lo[1]);
+  g.uyhi = (int)(wy ? p.uy[1] : b.hi[1]);
+  g.uzlo = (int)(wz ? p.uz[0] : b.lo[2]);
+  g.uzhi = (int)(wz ? p.uz[1] : b.hi[2]);
+  g.xlo_live = (int)-L.gx;
+  g.xhi_live = (int)(L.n[0] + L.gx - 1);
+  g.ylo_live = (int)-L.gy;
+  g.yhi_live = (int)(L.n[1] + L.gy - 1);
+  // every loaded column of every tile lies inside the row's allocation: the
+  // row starts zoff >= 16 elements before k = 0 (tiles start K <= 6 columns
+  // before the box) and the tail pad covers the last tile's overhang
+  HEAT3D_CHECK(b.lo[2] - K >= -L.zoff, "tl: tile columns before the row start");
+  HEAT3D_CHECK(g.uylo - 1 >= -L.gy && g.uyhi <= L.n[1] + L.gy && g.uylo <= b.lo[1] && g.uyhi >= b.hi[1] &&
+                   g.uzlo - 1 >= -L.gz && g.uzhi <= L.n[2] + L.gz && g.uzlo <= b.lo[2] && g.uzhi >= b.hi[2],
+               "tl: y/z update range outside the ghosted layout");
+  HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live + 1 && g.ulo <= b.lo[0] && g.uhi >= b.hi[0],
+               "tl: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
+  constexpr int ZS = 64 - 2 * K, YS = TY - 2 * K;
+  g.c00 = (int)(b.lo[2] - K);
+  g.r00 = (int)(b.lo[1] - K);
+  g.nzb = (int)std::max<int64_t>(1, (b.extent(2) + ZS - 1) / ZS);
+  g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
+  static const int slots =  // magic static: thread-safe under --gpus N
+      device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q>), 64 * WY);
+  const int64_t ntiles = (int64_t)g.nzb * g.nyb;
+  const int64_t nxb = b.extent(0);
+  constexpr int U = Q == 4 ? 12 : 6;  // the kernel's unroll (lcm(Q, 3, 2))
+  XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
+  HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
+  g.segsplit = xp.seg | (xp.split << 16);
+  g.n1 = xp.n1;
+  g.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
+  const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
+  HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
+  if (std::getenv("HEAT3D_TRACE"))
+    std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: seg=%d tiles=%dx%d blocks=%lld\n", K, (long long)nxb,
+                 xp.seg, g.nzb, g.nyb, (long long)nblocks);
+  HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl: residual slots " << p.slot << "+" << K);
+  static const int spill = [] {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q>)) == hipSuccess
+               ? (int)a.localSizeBytes
+               : 0;
+  }();
+  static const bool allow = std::getenv("HEAT3D_ALLOW_SPILL") && std::getenv("HEAT3D_ALLOW_SPILL")[0] == '1';
+  HEAT3D_CHECK(spill == 0 || allow, "tl variant " << ks.str() << " spills " << spill
+                                                  << " B of registers per lane (HEAT3D_ALLOW_SPILL=1 overrides)");
+  unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
+  const int* done = p.state ? &p.state->done : nullptr;
+  hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+                     static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0], (Real)p.D[1],
+                     (Real)p.D[2], r, done);
+  HIPK_CHECK(hipGetLastError());
+}
+
+template <typename Real>
+static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
+  const KernelSpec r = k.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
+  const int K = k.K, R = r.R, WY = r.WY, Q = r.NT;
+  HEAT3D_CHECK(r.V == 1 && r.WZ == 1, "tl kernels: one value per lane (V = 1), one wave across z (WZ = 1)");
+#define H3D_TBL(RR, YY, KK, QQ)                         \
+  if (R == RR && WY == YY && K == KK && Q == QQ) {      \
+    launch_tbl<Real, RR, YY, KK, QQ>(p, k, s);          \
+    return;                                             \
+  }
+  // 16 waves (<= 128 VGPRs, LDS 2K x 16 KiB): K <= 4; 12 waves (<= 168 VGPRs): K = 5
+  H3D_TBL(3, 16, 4, 3) H3D_TBL(3, 16, 4, 4) H3D_TBL(3, 16, 3, 3) H3D_TBL(3, 16, 3, 4)
+  H3D_TBL(2, 16, 4, 3) H3D_TBL(2, 16, 4, 4) H3D_TBL(2, 16, 5, 3) H3D_TBL(2, 16, 3, 3)
+  H3D_TBL(2, 16, 4, 6) H3D_TBL(2, 16, 3, 6) H3D_TBL(3, 16, 3, 6) H3D_TBL(2, 16, 2, 6)
+  H3D_TBL(3, 16, 2, 3) H3D_TBL(2, 16, 2, 3)
+  H3D_TBL(4, 12, 4, 3) H3D_TBL(4, 12, 4, 4) H3D_TBL(4, 12, 5, 3) H3D_TBL(3, 12, 5, 3)
+  if constexpr (sizeof(Real) == 4) {
+    // fp32: half the registers and LDS per row, so deeper sweeps fit 16 waves
+    H3D_TBL(4, 16, 4, 3) H3D_TBL(3, 16, 5, 3) H3D_TBL(4, 16, 5, 3) H3D_TBL(3, 16, 6, 3)
+    H3D_TBL(4, 16, 6, 3) H3D_TBL(4, 16, 4, 4) H3D_TBL(3, 16, 5, 6)
+  }
+#undef H3D_TBL
+  HEAT3D_THROW("unsupported tl kernel variant R=" << R << " WY=" << WY << " K=" << K << " Q=" << Q);
+}
+
+void stencil_lean(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
+  if (p.box.empty()) return;
+  if (t == DType::F64) dispatch_tbl<double>(p, k, S(stream));
+  else dispatch_tbl<float>(p, k, S(stream));
+}
+
+}  // namespace hip
+}  // namespace heat3d

@@ -521,9 +521,10 @@ void stencil_ring(DType t, const StencilParams& p, const KernelSpec& k, void* st
 void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
   switch (k.kind) {
     case KernelSpec::TBR: stencil_ring(t, p, k, stream); break;
+    case KernelSpec::TBL: stencil_lean(t, p, k, stream); break;
     case KernelSpec::TBK: stencil_multi(t, p, k, stream); break;
     case KernelSpec::TB2: stencil2(t, p, k, stream); break;
-    default: HEAT3D_THROW("sweep needs a multi-step kernel (tb2 | tbk2 | tb3..tb6 | tr2..tr6)");
+    default: HEAT3D_THROW("sweep needs a multi-step kernel (tb2 | tbk2 | tb3..tb6 | tr2..tr6 | tl2..tl6)");
   }
 }
 

@@ -72,14 +72,19 @@ KernelSpec KernelSpec::parse(const std::string& s) {
   } else if (parts[0] == "tile" || parts[0] == "tb2" || parts[0] == "tbk2" ||
              (parts[0].size() == 3 && parts[0][0] == 't' && parts[0][1] == 'b' && parts[0][2] >= '3' &&
               parts[0][2] <= '6') ||
-             (parts[0].size() == 3 && parts[0][0] == 't' && parts[0][1] == 'r' && parts[0][2] >= '2' &&
-              parts[0][2] <= '6')) {
+             (parts[0].size() == 3 && parts[0][0] == 't' && (parts[0][1] == 'r' || parts[0][1] == 'l') &&
+              parts[0][2] >= '2' && parts[0][2] <= '6')) {
     // tile = single step; tb2 = tuned 2-step kernel; tb3..tb6 / tbk2 = K-step
-    // queue kernel; tr2..tr6 = K-step register-ring kernel
-    k.kind = parts[0] == "tile" ? Tile : parts[0] == "tb2" ? TB2 : parts[0][1] == 'r' ? TBR : TBK;
+    // queue kernel; tr2..tr6 = K-step register-ring kernel; tl2..tl6 = lean
+    // K-step kernel
+    k.kind = parts[0] == "tile" ? Tile
+             : parts[0] == "tb2" ? TB2
+             : parts[0][1] == 'r' ? TBR
+             : parts[0][1] == 'l' ? TBL
+                                  : TBK;
     if (k.kind == TB2) k.K = 2;
     if (k.kind == TBK) k.K = parts[0] == "tbk2" ? 2 : parts[0][2] - '0';
-    if (k.kind == TBR) k.K = parts[0][2] - '0';
+    if (k.kind == TBR || k.kind == TBL) k.K = parts[0][2] - '0';
     auto at = [&](std::size_t i) { return parts.size() > i ? std::atoi(parts[i].c_str()) : 0; };
     k.V = at(1);
     k.R = at(2);
@@ -90,7 +95,8 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     if (k.kind == TBR && parts.size() > 7) k.O = at(7);  // 1 = non-temporal output stores
   } else {
     throw UsageError("unknown kernel '" + s +
-                     "' (auto | naive | column[:V[:R[:L[:O[:NT]]]]] | tile|tb2..tb6|tbk2[:V[:R[:WZ[:WY[:L[:NT]]]]]])");
+                     "' (auto | naive | column[:V[:R[:L[:O[:NT]]]]] | tile|tb2..tb6|tbk2|tr2..tr6|tl2..tl6"
+                     "[:V[:R[:WZ[:WY[:L[:NT]]]]]])");
   }
   return k;
 }
@@ -136,6 +142,15 @@ KernelSpec KernelSpec::resolved(DType t) const {
       def(r.WY, f64 ? (K <= 3 ? 16 : 8) : 8);
       def(r.NT, 3);
       break;
+    case TBL:  // lean kernel: 16 waves of 64 columns.  fp64: 3 rows per wave
+               // (48-row tiles), 2 from K = 4 (32-row tiles: 115 VGPRs, no
+               // spill); fp32: 4 rows from K = 4 (64-row tiles)
+      def(r.V, 1);
+      def(r.R, f64 ? (K >= 4 ? 2 : 3) : (K >= 4 && K <= 5 ? 4 : 3));
+      def(r.WZ, 1);
+      def(r.WY, 16);
+      def(r.NT, 3);
+      break;
     default:
       break;
   }
@@ -149,6 +164,7 @@ std::string KernelSpec::str() const {
     os << (kind == Tile  ? std::string("tile:")
            : kind == TB2 ? std::string("tb2:")
            : kind == TBR ? "tr" + std::to_string(K) + ":"
+           : kind == TBL ? "tl" + std::to_string(K) + ":"
            : K == 2      ? std::string("tbk2:")
                          : "tb" + std::to_string(K) + ":")
        << V << ":" << R << ":" << WZ << ":" << WY << ":" << L << ":" << NT;
@@ -191,11 +207,15 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   // Auto depth: 3, for one subdomain and for x slabs alike (MI355X, 1024^3
   // fp64 as 8 virtual x slabs on one GPU: K = 3 341 GLUPS vs K = 2 301 with the
   // ring kernel; profiles/kernel_sweep.md)
-  int K = cfg_.temporal >= 2 ? cfg_.temporal : kspec2_.multi_step() ? kspec2_.K : kDefaultTemporal;
-  // default kernel: the register-ring kernel (stencil_tbr.hip; 1024^3 fp64
-  // tr3 621-640 vs tb3 551 GLUPS, fp32 1090 vs 884), except at K = 2 where the
-  // tuned queue kernel tb2 is faster (508 vs 490); tb2 / tbK / trK force one
-  if (!kspec2_.multi_step()) kspec2_.kind = K == 2 ? KernelSpec::TB2 : KernelSpec::TBR;
+  int K = cfg_.temporal >= 2 ? cfg_.temporal
+          : kspec2_.multi_step() ? kspec2_.K
+          : dt_ == DType::F64    ? kDefaultTemporal
+                                 : kDefaultTemporalF32;
+  // default kernel: the lean kernel (stencil_tbl.hip; MI355X 1024^3, same box:
+  // fp64 tl3 740-746 vs ring tr3 726-732 GLUPS, fp32 tl4 1168 vs tr3 1125),
+  // except at K = 2 where the tuned queue kernel tb2 is used; tb2 / tbK /
+  // trK / tlK force one
+  if (!kspec2_.multi_step()) kspec2_.kind = K == 2 ? KernelSpec::TB2 : KernelSpec::TBL;
   if (kspec2_.kind == KernelSpec::TB2 && K != 2) kspec2_.kind = KernelSpec::TBK;
   kspec2_.K = K;
   int64_t min_n[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
@@ -207,9 +227,10 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   for (int a = 0; a < 3; ++a) fits &= dims[a] == 1 || min_n[a] >= K;
   tb_ = kspec_.kind != KernelSpec::Naive && (cfg_.temporal >= 2 || (cfg_.temporal == 0 && be_->is_gpu())) && fits;
   if (tb_ && block) {
-    if (cfg_.kernel2.empty() || cfg_.kernel2 == "auto") kspec2_.kind = KernelSpec::TBR;
-    if (kspec2_.kind != KernelSpec::TBR)
-      throw UsageError("temporal blocking with y/z neighbours needs a register-ring kernel (--kernel2 trK)");
+    if (cfg_.kernel2.empty() || cfg_.kernel2 == "auto") kspec2_.kind = KernelSpec::TBL;
+    if (kspec2_.kind != KernelSpec::TBR && kspec2_.kind != KernelSpec::TBL)
+      throw UsageError("temporal blocking with y/z neighbours needs a kernel with y/z update ranges "
+                       "(--kernel2 trK or tlK)");
   }
   K_ = tb_ ? K : 1;
   for (int a = 0; a < 3; ++a) hd_[a] = tb_ && dims[a] > 1 ? K : 1;
@@ -598,8 +619,10 @@ void Solver::enqueue_iteration(int p, int bi) {
 // q+2 onwards are no-ops.  Exchanged values stay bitwise identical.
 void Solver::enqueue_multi(int bi, int Kp) {
   // Kp < K_: a partial sweep of Kp steps (the remainder of a step count that
-  // is not a multiple of K_), same schedule and buffers, ring kernel of depth Kp
+  // is not a multiple of K_), same schedule and buffers, kernel of depth Kp;
+  // Kp = K_ + 1: a long sweep (long_sweeps_for, single subdomain only)
   if (Kp <= 0) Kp = K_;
+  HEAT3D_CHECK(Kp <= K_ || (Kp == K_ + 1 && !has_halo_), "sweep depth " << Kp << " exceeds the halo depth " << K_);
   H3D_TRACE("sweep" << Kp << " issued=" << issued_ << " buf=" << bi << (capturing_ ? " (capturing)" : ""));
   HEAT3D_CHECK(tb_, "temporal blocking not enabled for this decomposition");
   if (last_kind_ != 2) join_pipeline();
@@ -609,8 +632,10 @@ void Solver::enqueue_multi(int bi, int Kp) {
   const int slot0 = lag_ ? q * K_ : 0;
   KernelSpec ks = kspec2_;
   if (Kp != K_) {
+    // partial (Kp < K) or long (Kp = K + 1, single subdomain) sweep: the
+    // kernel family's default variant of depth Kp
     ks = KernelSpec();
-    ks.kind = KernelSpec::TBR;
+    ks.kind = kspec2_.kind == KernelSpec::TBL ? KernelSpec::TBL : KernelSpec::TBR;
     ks.K = Kp;
   }
   // update ranges reach Kp - 1 (not K_ - 1) points into the deep halos
@@ -803,6 +828,18 @@ int Solver::graph_len_for(int64_t n) const {
   return G;
 }
 
+int Solver::long_sweeps_for(int64_t n) const {
+  if (!tb_ || has_halo_ || kspec2_.kind != KernelSpec::TBL || n % K_ == 0) return 0;
+  if (K_ + 1 > 6 || K_ + 1 > kResidualSlots) return 0;
+  const int64_t b = n % K_;             // n = a K + b (K + 1) with a = (n - b (K + 1)) / K
+  if (b * (K_ + 1) > n) return 0;
+  static const bool off = [] {
+    const char* e = std::getenv("HEAT3D_LONG_SWEEPS");
+    return e && e[0] == '0';
+  }();
+  return off ? 0 : (int)b;
+}
+
 bool Solver::graphs_allowed() const {
   // Multi-stream (overlapped) schedules are graphs too (built explicitly by
   // the backend's recorder); HEAT3D_GRAPH_MULTISTREAM=0 restricts graphs to
@@ -917,12 +954,15 @@ Solver::GraphEntry* Solver::build_graph(int G) {
 
 void Solver::prepare_steps(int64_t n) {
   if (!graphs_allowed()) return;
-  const int G = graph_len_for(n);
+  const int G = graph_len_for(n - (int64_t)long_sweeps_for(n) * (K_ + 1));
   if (G > 0 && !find_graph(G)) build_graph(G);
 }
 
 void Solver::run_chunk(int64_t n) {
   const bool graphs = graphs_allowed();
+  // remainder as long sweeps, issued after the graph-sized part
+  const int nlong = long_sweeps_for(n);
+  n -= (int64_t)nlong * (K_ + 1);
   while (n > 0) {
     const int G = graphs ? graph_len_for(n) : 0;
     if (G > 0) {
@@ -977,6 +1017,12 @@ void Solver::run_chunk(int64_t n) {
     ++issued_;
     cur_ = nxt(cur_);
     --n;
+  }
+  for (int i = 0; i < nlong; ++i) {
+    record_segment(issued_, K_ + 1, cur());
+    enqueue_multi(cur(), K_ + 1);
+    issued_ += K_ + 1;
+    cur_ = nxt(cur_);
   }
   flush_pending_reduce();
 }

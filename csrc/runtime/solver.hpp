@@ -33,8 +33,12 @@
 namespace heat3d {
 
 // Temporal blocking depth used when neither --temporal K nor --kernel2 tbK
-// names one.
+// names one: fp64 3 (the lean kernel is HBM-bound at K = 3; K = 4 does not
+// fit 16 waves x 128 VGPRs with 48-row tiles), fp32 4 (half the registers per
+// row: 64-row tiles; K = 5 is within 1% but needs 2K = 10 residual slots for
+// the lagged check of overlapped sweeps; profiles/kernel_sweep.md).
 constexpr int kDefaultTemporal = 3;
+constexpr int kDefaultTemporalF32 = 4;
 
 struct RunResult {
   bool converged = false;
@@ -186,6 +190,10 @@ class Solver {
   void flush_pending_reduce();
   bool graphs_allowed() const;
   int graph_len_for(int64_t n) const;
+  // Sweeps of depth K+1 that absorb the remainder of a chunk of n steps that
+  // is not a multiple of K (single subdomain, lean kernel): n = a K + b (K+1)
+  // costs a + b HBM passes where a K-sweep + a partial one would cost one more.
+  int long_sweeps_for(int64_t n) const;
   bool multi_stream() const { return tb_ ? tb_overlap_ : overlap_; }
   // buffer holding T^{issued_}; a step or a K-step sweep reads cur() and
   // writes nxt(cur())

@@ -104,9 +104,13 @@ def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
 
 
 VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb3:1:4:1:16", "tb3:1:6:1:8", "tb3:1:4:2:8", "tb3:1:4:1:8:3",
-                  "tr3", "tr3:1:3:1:16:0:3", "tr3:1:4:1:8:0:4", "tr3:1:6:1:8:0:3", "tr3:1:4:1:8:5:3", "tr3:1:2:1:16:0:3"],
-              4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1", "tr4", "tr4:1:4:1:8:0:3", "tr4:1:4:1:8:0:4"],
-              2: ["tbk2", "tbk2:2:2:1:8", "tr2", "tr2:2:2:1:8:0:3", "tr2:1:4:1:16:0:3", "tr2:1:2:1:16"]}
+                  "tr3", "tr3:1:3:1:16:0:3", "tr3:1:4:1:8:0:4", "tr3:1:6:1:8:0:3", "tr3:1:4:1:8:5:3", "tr3:1:2:1:16:0:3",
+                  "tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5:3", "tl3:1:3:1:16:0:6",
+                  "tl3:1:2:1:16:7:6"],
+              4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1", "tr4", "tr4:1:4:1:8:0:3", "tr4:1:4:1:8:0:4",
+                  "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6"],
+              2: ["tbk2", "tbk2:2:2:1:8", "tr2", "tr2:2:2:1:8:0:3", "tr2:1:4:1:16:0:3", "tr2:1:2:1:16",
+                  "tl2", "tl2:1:2:1:16:0:3"]}
 VARIANTS_K_F32 = {3: ["tr3:2:4:1:8:0:3", "tr3:2:4:1:8:0:4", "tr3:2:4:1:16:0:3"], 4: ["tr4:2:4:1:8:0:4"],
                   2: ["tr2:2:4:1:8:0:3", "tr2:2:4:1:8:0:4"]}
 
@@ -167,7 +171,8 @@ def _deep_random(ops, n, gx, dtype, seed):
 
 
 @pytest.mark.parametrize("kernel", ["tb2", "tbk2", "tb3", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb4", "tb4:1:6:1:8",
-                                    "tr2", "tr3", "tr3:1:3:1:16:0:3", "tr4", "tr2:2:2:1:8:0:3"])
+                                    "tr2", "tr3", "tr3:1:3:1:16:0:3", "tr4", "tr2:2:2:1:8:0:3",
+                                    "tl2", "tl3", "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:0:6"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (5, (0, 5), "lo"), (9, (0, 9), "hi"),
                                             (12, (4, 8), "both"), (12, (0, 4), "both"), (12, (8, 12), "both"),
@@ -219,7 +224,7 @@ def test_temporal_mixed_steps_gpu(h3d, gpu, K, vr):
     assert np.array_equal(a.gather(), b.gather())
 
 
-@pytest.mark.parametrize("kernel2", ["tr3", "tr3:1:4:1:8:0:3", "tr2", "tr4"])
+@pytest.mark.parametrize("kernel2", ["tr3", "tr3:1:4:1:8:0:3", "tr2", "tr4", "tl3", "tl4", "tl2"])
 @pytest.mark.parametrize("vr", [1, 3])
 def test_ring_kernel_solver_gpu(h3d, gpu, kernel2, vr):
     """Register-ring sweeps (stencil_tbr.hip) in the solver, single domain and
@@ -234,7 +239,7 @@ def test_ring_kernel_solver_gpu(h3d, gpu, kernel2, vr):
     assert np.array_equal(a.gather(), b.gather())
 
 
-@pytest.mark.parametrize("kernel2", ["tr3", "tr2", "tb3", "tb2"])
+@pytest.mark.parametrize("kernel2", ["tr3", "tr2", "tb3", "tb2", "tl3", "tl4"])
 def test_sweep_nan_faults(h3d, gpu, kernel2):
     """A NaN anywhere in the field reaches the convergence check as a fault
     (the ring kernel detects it on the stored T^{n+K} and poisons every slot)."""
@@ -249,7 +254,8 @@ def test_sweep_nan_faults(h3d, gpu, kernel2):
 
 @pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2), (2, 1, 3), (1, 3, 1), (1, 1, 2)])
 @pytest.mark.parametrize("kernel2,dtype", [("tr3", "fp64"), ("tr2", "fp64"), ("tr4", "fp64"),
-                                           ("tr3:1:6:1:8:0:3", "fp64"), ("tr3", "fp32"), ("tr4:1:4:1:8:0:3", "fp32")])
+                                           ("tr3:1:6:1:8:0:3", "fp64"), ("tr3", "fp32"), ("tr4:1:4:1:8:0:3", "fp32"),
+                                           ("tl3", "fp64"), ("tl4", "fp64"), ("tl4", "fp32")])
 def test_block_decomposition_ring_kernel_gpu(h3d, gpu, dims, kernel2, dtype):
     """Deep y / z halos (axis-ordered exchange with edges and corners) and the
     ring kernel's y / z update ranges: virtual-rank block decompositions on
@@ -286,7 +292,8 @@ def _deep3_random(ops, n, g, dtype, seed):
     return f
 
 
-@pytest.mark.parametrize("kernel", ["tr2", "tr3", "tr4", "tr3:1:6:1:8:0:3", "tr3:1:3:1:16:0:3:1"])
+@pytest.mark.parametrize("kernel", ["tr2", "tr3", "tr4", "tr3:1:6:1:8:0:3", "tr3:1:3:1:16:0:3:1",
+                                    "tl2", "tl3", "tl4", "tl3:1:3:1:16:0:4"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("box,sides", [((0, 12, 0, 50, 0, 140), "lo"), ((0, 12, 0, 50, 0, 140), "hi"),
                                        ((0, 12, 0, 50, 0, 140), "both"), ((0, 12, 4, 46, 0, 140), "both"),

@@ -79,10 +79,14 @@ def test_single_plane_slabs_fall_back(h3d):
     assert not s.native.temporal_blocking
 
 
-def test_block_decomposition_uses_ring_kernel(h3d):
-    # y / z splits take temporal blocking too, with the register-ring kernel
+def test_block_decomposition_uses_lean_kernel(h3d):
+    # y / z splits take temporal blocking too, with a kernel that has y / z
+    # update ranges: the lean kernel by default, the ring kernel on request
     s = h3d.HeatSolver((17, 17, 17), 10, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1), extra_args=T2)
     assert s.native.temporal_blocking and s.native.temporal_steps == 2
+    assert s.native.kernel_name.startswith("tl2"), s.native.kernel_name
+    s = h3d.HeatSolver((17, 17, 17), 10, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1),
+                       extra_args=T2 + ["--kernel2", "tr2"])
     assert s.native.kernel_name.startswith("tr2"), s.native.kernel_name
 
 

@@ -1,6 +1,9 @@
 #!/bin/bash
 # rocprofv3 PMC passes over tools/tune.py (one counter group per run, each under
-# its own hard time limit).  Usage: tools/pmc_passes.sh OUTDIR VARIANT [N] [DTYPE]
+# its own hard time limit; counter-slot limits of gfx950 respected: <= 8 SQ,
+# <= 4 TCC, <= 2 TA per pass).  Counters are per dispatch: every row of the
+# summary is one 1024^3 sweep (tools/summarize_rocprof.py takes the median).
+# Usage: tools/pmc_passes.sh OUTDIR VARIANT [N] [DTYPE]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -9,8 +12,10 @@ out=$1; var=$2; n=${3:-1024}; dt=${4:-fp64}
 case "$out" in /*) ;; *) out="$ROOT/$out" ;; esac
 mkdir -p "$out"
 passes=(
-  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU"
-  "SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE GRBM_COUNT"
+  "SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS"
+  "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_LEVEL_VMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"
+  "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"
+  "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_64B_sum GRBM_GUI_ACTIVE"
   "FETCH_SIZE"
   "WRITE_SIZE"
 )

@@ -52,7 +52,7 @@ def main():
     res = {v: [] for v in a.variants}
     def steps(v):  # time steps per sweep of a variant
         head = v.split(":")[0]
-        return 2 if head in ("tb2", "tbk2") else int(head[2]) if head[:2] in ("tb", "tr") else 1
+        return 2 if head in ("tb2", "tbk2") else int(head[2]) if head[:2] in ("tb", "tr", "tl") else 1
 
     def run(v, a_, b_):
         (ops.ftcs_step2 if steps(v) > 1 else ops.ftcs_step)(a_, b_, D, kernel=v, state=state)
