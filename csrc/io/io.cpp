@@ -1,5 +1,6 @@
 #include "io.hpp"
 
+#include <dirent.h>
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -174,20 +175,60 @@ std::string read_file(const std::string& path) {
 
 void write_file_atomic(const std::string& path, const std::string& content) {
   make_dirs(dirname_of(path));
-  std::string tmp = path + ".tmp";
-  {
-    std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
-    if (!f) HEAT3D_THROW("cannot write '" << tmp << "'");
-    f << content;
-  }
-  if (std::rename(tmp.c_str(), path.c_str()) != 0) HEAT3D_THROW("rename to '" << path << "' failed");
+  const std::string tmp = path + ".tmp";
+  int fd = open_raw(tmp, true, true);
+  pwrite_all(fd, content.data(), content.size(), 0);
+  fsync_raw(fd);
+  close_raw(fd);
+  rename_durable(tmp, path);
 }
 
-int open_raw(const std::string& path, bool write) {
-  int fd = write ? ::open(path.c_str(), O_WRONLY | O_CREAT, 0644) : ::open(path.c_str(), O_RDONLY);
+int open_raw(const std::string& path, bool write, bool truncate) {
+  int fd = write ? ::open(path.c_str(), O_WRONLY | O_CREAT | (truncate ? O_TRUNC : 0), 0644)
+                 : ::open(path.c_str(), O_RDONLY);
   if (fd < 0) HEAT3D_THROW("open(" << path << ") failed: " << std::strerror(errno));
   return fd;
 }
+
+void truncate_raw(int fd, int64_t size) {
+  if (::ftruncate(fd, size) != 0) HEAT3D_THROW("ftruncate failed: " << std::strerror(errno));
+}
+
+void fsync_raw(int fd) {
+  if (::fsync(fd) != 0 && errno != EINVAL) HEAT3D_THROW("fsync failed: " << std::strerror(errno));
+}
+
+int64_t file_size(const std::string& path) {
+  struct stat st;
+  if (::stat(path.c_str(), &st) != 0) return -1;
+  return (int64_t)st.st_size;
+}
+
+void rename_durable(const std::string& from, const std::string& to) {
+  if (std::rename(from.c_str(), to.c_str()) != 0)
+    HEAT3D_THROW("rename '" << from << "' -> '" << to << "' failed: " << std::strerror(errno));
+  std::string d = dirname_of(to);
+  if (d.empty()) d = ".";
+  int fd = ::open(d.c_str(), O_RDONLY | O_DIRECTORY);
+  if (fd >= 0) {
+    (void)::fsync(fd);
+    ::close(fd);
+  }
+}
+
+std::vector<std::string> list_dir(const std::string& dir) {
+  std::vector<std::string> out;
+  DIR* d = ::opendir(dir.c_str());
+  if (!d) return out;
+  while (dirent* e = ::readdir(d)) {
+    const std::string n = e->d_name;
+    if (n != "." && n != "..") out.push_back(n);
+  }
+  ::closedir(d);
+  return out;
+}
+
+void remove_file(const std::string& path) { (void)std::remove(path.c_str()); }
 
 void pwrite_all(int fd, const void* p, std::size_t n, int64_t off) {
   const char* c = static_cast<const char*>(p);

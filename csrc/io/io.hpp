@@ -58,7 +58,15 @@ std::string read_file(const std::string& path);
 void write_file_atomic(const std::string& path, const std::string& content);
 
 // Raw global-grid file access (positioned I/O, any process, disjoint ranges).
-int open_raw(const std::string& path, bool write);
+// truncate = create / empty the file (one process, before the others open it).
+int open_raw(const std::string& path, bool write, bool truncate = false);
+void truncate_raw(int fd, int64_t size);
+void fsync_raw(int fd);
+int64_t file_size(const std::string& path);  // -1 if missing
+// rename + fsync of the directory entry
+void rename_durable(const std::string& from, const std::string& to);
+std::vector<std::string> list_dir(const std::string& dir);
+void remove_file(const std::string& path);
 void pwrite_all(int fd, const void* p, std::size_t n, int64_t off);
 void pread_all(int fd, void* p, std::size_t n, int64_t off);
 void close_raw(int fd);

@@ -789,6 +789,25 @@ void check_convergence(DeviceState* s, int slot, void* stream, int count) {
   HIPK_CHECK(hipGetLastError());
 }
 
+// Placement probe: every workgroup records (XCC id, SE / SH / CU id) of the
+// CU it ran on (s_getreg of HW_REG_XCC_ID and HW_REG_HW_ID bits [15:8]), after
+// spinning `ticks` so that the grid spreads over every CU it may use.
+__global__ void cu_probe_kernel(unsigned* out, unsigned long long ticks) {
+  if (threadIdx.x == 0) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20); // HW_REG_XCC_ID
+    out[blockIdx.x] = ((xcc & 0xf) << 8) | ((hw >> 8) & 0xff);
+  }
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+void cu_probe(unsigned* out, int blocks, double us, void* stream) {
+  hipLaunchKernelGGL(cu_probe_kernel, dim3((unsigned)blocks), dim3(64), 0, S(stream), out,
+                     (unsigned long long)(us * 100.0));
+  HIPK_CHECK(hipGetLastError());
+}
+
 __global__ void delay_kernel(unsigned long long ticks) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);

@@ -12,8 +12,11 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+
+#include <hip/hip_runtime.h>
 
 #include "../comm/comm.hpp"
 #include "../comm/net.hpp"
@@ -168,6 +171,30 @@ PYBIND11_MODULE(_heat3d, m) {
   m.def("device_count", &hip_device_count);
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
+  // Which CUs a stream created with a CU mask reaches: runs the placement
+  // probe on hipExtStreamCreateWithCUMask(mask) (an empty mask: a plain
+  // stream) and returns the distinct (XCC << 8 | SE/SH/CU) ids seen.
+  m.def("cu_mask_probe", [](int device, std::vector<uint32_t> mask, int blocks) {
+    if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
+    hipStream_t st = nullptr;
+    if (mask.empty()) {
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) throw std::runtime_error("stream");
+    } else if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+      throw std::runtime_error("hipExtStreamCreateWithCUMask failed");
+    }
+    unsigned* d = nullptr;
+    if (hipMalloc(&d, sizeof(unsigned) * blocks) != hipSuccess) throw std::runtime_error("hipMalloc");
+    heat3d::hip::cu_probe(d, blocks, 50.0, st);
+    std::vector<unsigned> h(blocks);
+    if (hipMemcpyAsync(h.data(), d, sizeof(unsigned) * blocks, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      throw std::runtime_error("probe failed");
+    (void)hipFree(d);
+    (void)hipStreamDestroy(st);
+    std::sort(h.begin(), h.end());
+    h.erase(std::unique(h.begin(), h.end()), h.end());
+    return h;
+  }, py::arg("device"), py::arg("mask"), py::arg("blocks") = 8192);
   // Executes RcclComm::exchange / allreduce on a one-rank communicator: every
   // transfer is a send and a receive to self inside one RCCL group (sizes that
   // are and are not multiples of 8 bytes), plus a padded K-deep x halo plane of

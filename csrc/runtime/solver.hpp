@@ -121,6 +121,8 @@ class Solver {
 
   // Output / checkpoint.
   void write_tecplot(const std::string& path, const std::string& layout);
+  // per-rank zones ("owned" layout), written in parallel at computed offsets
+  void write_tecplot_zones(const std::string& path);
   void save_checkpoint(const std::string& dir);
   void load_checkpoint(const std::string& dir);
 
@@ -188,6 +190,7 @@ class Solver {
   // lagged overlapped sweeps: the all-reduce of sweep q is issued after the
   // halo of sweep q+1 (see enqueue_multi); flush issues a pending one
   void flush_pending_reduce();
+  unsigned long long allreduce_sum_u64(unsigned long long v);
   bool graphs_allowed() const;
   int graph_len_for(int64_t n) const;
   // Sweeps of depth K+1 that absorb the remainder of a chunk of n steps that

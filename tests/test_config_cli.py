@@ -133,8 +133,10 @@ def test_threads_per_rank_cli(heat3d_bin, tmp_path, gpus, decomp, temporal):
     assert b["ranks"] == gpus and b["comm"] == "socket"
     assert a["conv_iter"] == b["conv_iter"] and abs(a["error_percent"] - b["error_percent"]) < 1e-12
     assert many.stdout.count("Runnung HeatEquation3D") == 1  # one report per job, not per thread
-    ra = np.fromfile(tmp_path / "c1" / "field.raw", dtype=np.float64)
-    rb = np.fromfile(tmp_path / "cn" / "field.raw", dtype=np.float64)
+    fa = json.loads((tmp_path / "c1" / "meta.json").read_text())["field"]
+    fb = json.loads((tmp_path / "cn" / "meta.json").read_text())["field"]
+    ra = np.fromfile(tmp_path / "c1" / fa, dtype=np.float64)
+    rb = np.fromfile(tmp_path / "cn" / fb, dtype=np.float64)
     assert np.array_equal(ra, rb)
 
 

@@ -31,7 +31,10 @@ def test_native_socket_matches_single_process(h3d, tmp_path, world, decomp):
     assert abs(float(err) - r1["error_percent"]) < 1e-12
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
     # checkpoint written cooperatively by all ranks equals the single-process field
-    raw = np.fromfile(tmp_path / "ckpt" / "field.raw", dtype=np.float64).reshape(n, n, n)
+    import json
+
+    meta = json.loads((tmp_path / "ckpt" / "meta.json").read_text())
+    raw = np.fromfile(tmp_path / "ckpt" / meta["field"], dtype=np.float64).reshape(n, n, n)
     assert np.array_equal(raw, single.gather())
     # owned-layout Tecplot zones tile the grid: one zone per rank
     zones = h3d.utils.read_tecplot(str(tmp_path / "out.dat"))["zones"]

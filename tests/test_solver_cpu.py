@@ -173,3 +173,69 @@ def test_phantom_rank_proxy_runs(h3d, rank, size, decomp, temporal, monkeypatch)
     s.synchronize()
     st = s.state()
     assert st["iter"] == 13 and st["done"] == 0, st
+
+
+def test_checkpoint_crash_safety_and_checksum(h3d, tmp_path):
+    """Checkpoints are crash-safe (field.<iter>.raw written to a temp file,
+    fsync'd and renamed before meta.json is atomically switched to it; older
+    fields removed) and verified on restart (size + checksum)."""
+    import json
+
+    ck = tmp_path / "ck"
+    a = h3d.HeatSolver((19, 17, 21), 40, 0.0, backend="cpu", virtual_ranks=3)
+    a.run()
+    a.save_checkpoint(str(ck))
+    a.step(7)
+    a.save_checkpoint(str(ck))
+    meta = json.loads((ck / "meta.json").read_text())
+    assert meta["format"] == "heat3d-checkpoint-v2" and meta["iteration"] == 47
+    assert meta["field"] == "field.47.raw" and meta["bytes"] == 19 * 17 * 21 * 8
+    assert sorted(p.name for p in ck.iterdir()) == ["field.47.raw", "meta.json"]
+    raw = np.fromfile(ck / meta["field"], dtype=np.uint64)
+    assert f"{int(raw.sum(dtype=np.uint64)):016x}" == meta["checksum"]
+    assert np.array_equal(raw.view(np.float64).reshape(19, 17, 21), a.gather())
+    # a restart on another decomposition resumes the same trajectory
+    b = h3d.HeatSolver((19, 17, 21), 60, 0.0, backend="cpu", virtual_ranks=2,
+                       extra_args=["--restart", str(ck)])
+    c = h3d.HeatSolver((19, 17, 21), 60, 0.0, backend="cpu")
+    b.run(), c.run()
+    assert np.array_equal(b.gather(), c.gather())
+    # a corrupted (or half-written) field is refused, not silently loaded
+    buf = bytearray((ck / meta["field"]).read_bytes())
+    buf[8 * 2000] ^= 0x10
+    (ck / meta["field"]).write_bytes(bytes(buf))
+    with pytest.raises(Exception, match="checksum"):
+        h3d.HeatSolver((19, 17, 21), 60, 0.0, backend="cpu", extra_args=["--restart", str(ck)]).run()
+    (ck / meta["field"]).write_bytes(bytes(buf[:-8]))
+    with pytest.raises(Exception, match="bytes"):
+        h3d.HeatSolver((19, 17, 21), 60, 0.0, backend="cpu", extra_args=["--restart", str(ck)]).run()
+
+
+def test_streamed_io_bounded_chunks(h3d, tmp_path, monkeypatch):
+    """With a 1 MiB staging chunk the checkpoint, the per-rank Tecplot zones
+    and the root gather stream in many chunks and give the same bytes."""
+    import filecmp
+
+    s = h3d.HeatSolver((37, 29, 33), 30, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1))
+    s.run()
+    s.write_tecplot(str(tmp_path / "a.dat"), "owned")
+    s.save_checkpoint(str(tmp_path / "ca"))
+    g = s.gather()
+    monkeypatch.setenv("HEAT3D_IO_STAGE_MB", "1")
+    t = h3d.HeatSolver((37, 29, 33), 30, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1))
+    t.run()
+    t.write_tecplot(str(tmp_path / "b.dat"), "owned")
+    t.save_checkpoint(str(tmp_path / "cb"))
+    assert filecmp.cmp(tmp_path / "a.dat", tmp_path / "b.dat", shallow=False)
+    assert filecmp.cmp(tmp_path / "ca" / "field.30.raw", tmp_path / "cb" / "field.30.raw", shallow=False)
+    assert np.array_equal(t.gather(), g)
+    zones = h3d.utils.read_tecplot(str(tmp_path / "b.dat"))["zones"]
+    assert len(zones) == 4 and sum(np.prod(z["shape"]) for z in zones) == 37 * 29 * 33
+
+
+def test_gather_refuses_oversized_grid(h3d, monkeypatch):
+    s = h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu")
+    s.run()
+    monkeypatch.setenv("HEAT3D_HOST_MEM_LIMIT_GB", "0.0001")
+    with pytest.raises(Exception, match="host memory"):
+        s.gather()
