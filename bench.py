@@ -227,6 +227,7 @@ def run_rank(args) -> int:
     comm_ranks = s.native.comm_transport_ranks
     K = s.native.temporal_steps
     nbuf = s.native.field_buffers
+    reserved = s.native.reserved_cus
     placement = all_gather_objects({"rank": rank, "device": dev, "host": socket.gethostname(),
                                     "subdomain": list(s.native.local_subdomain(0)["n"])}, group)
     del s
@@ -267,7 +268,7 @@ def run_rank(args) -> int:
                    "kernel": kernel, "temporal_K": K, "field_buffers": nbuf,
                    "graph_requested": not args.no_graph, "graph_used": graph_launches > 0,
                    "graph_launches": graph_launches,
-                   "overlap": not args.no_overlap, "comm": comm_name},
+                   "overlap": not args.no_overlap, "comm": comm_name, "reserved_cus": reserved},
         "comm_ranks": comm_ranks,
         "placement": placement,
         "halo_verified": True,

@@ -106,6 +106,9 @@ std::string Config::usage() {
      << "  --timers                  per-phase GPU timing (synchronised diagnostic run)\n"
      << "  --verbose N               print residual every N iterations\n"
      << "  --threads N               CPU backend OpenMP threads\n"
+     << "  --reserve-cus N           CUs kept free of the interior sweep for comm / boundary / check\n"
+     << "                            kernels (default: 8 = one per XCD when the overlapped\n"
+     << "                            multi-rank schedule runs, else 0)\n"
      << "  --quiet                   suppress the banner\n";
   return os.str();
 }
@@ -199,6 +202,7 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--json-out") c.json_out = get("--json-out");
     else if (key == "--verbose") c.verbose = (int)to_i64(get("--verbose"), "--verbose");
     else if (key == "--threads") c.cpu_threads = (int)to_i64(get("--threads"), "--threads");
+    else if (key == "--reserve-cus") c.reserve_cus = (int)to_i64(get("--reserve-cus"), "--reserve-cus");
     else if (key == "--quiet") c.quiet = true;
     else if (key == "--help") throw UsageError("help requested");
     else throw UsageError("unknown option '" + a + "'");

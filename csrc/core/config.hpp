@@ -68,6 +68,7 @@ struct Config {
   int verbose = 0;
   bool quiet = false;
   int cpu_threads = 0;
+  int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules
 
   // Parse argv.  Throws UsageError on a malformed command line.
   static Config parse(int argc, const char* const* argv);

@@ -639,6 +639,7 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("graph_launches", &Solver::graph_launches)
       .def_property_readonly("comm_transport_ranks", [](Solver& s) { return s.comm().transport_ranks(); })
       .def_property_readonly("device", [](Solver& s) { return s.backend().device(); })
+      .def_property_readonly("reserved_cus", [](Solver& s) { return s.backend().reserved_cus(); })
       .def_property_readonly("kernel_name", &Solver::kernel_name)
       .def_property_readonly("temporal_blocking", &Solver::temporal_blocking)
       .def_property_readonly("temporal_steps", &Solver::temporal_steps)

@@ -38,6 +38,13 @@ class Backend {
   virtual void memset(void* dst, int v, std::size_t bytes, StreamId s) = 0;
 
   virtual void* stream(StreamId s) = 0;  // native handle (hipStream_t) or nullptr
+  // Keep n CUs free of compute-stream work (HIP: the compute stream is
+  // re-created with a CU mask; mask bit i is a CU of XCD i mod 8, so n = 8
+  // reserves one CU per XCD) so that comm / boundary / check kernels of the
+  // overlapped schedule start at once instead of waiting for a retiring
+  // workgroup of the interior sweep.  Call before any work is enqueued.
+  virtual void reserve_cus(int /*n*/) {}
+  virtual int reserved_cus() const { return 0; }
   // Bracket work that a caller enqueues itself on stream s (RCCL calls):
   // op_begin returns the native stream to enqueue on — the real stream, or,
   // while a graph is being recorded, a private stream capturing this one

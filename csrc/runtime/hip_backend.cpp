@@ -121,6 +121,22 @@ class HipBackend final : public Backend {
   }
 
   void* stream(StreamId s) override { return streams_[s]; }
+  void reserve_cus(int n) override {
+    if (n <= 0 || n == reserved_) return;
+    int cus = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_));
+    HEAT3D_CHECK(n < cus, "cannot reserve " << n << " of " << cus << " CUs");
+    const int words = (cus + 31) / 32;
+    std::vector<uint32_t> mask(words, 0u);
+    for (int i = 0; i < cus - n; ++i) mask[i / 32] |= 1u << (i % 32);  // clear the top n bits
+    hipStream_t s = nullptr;
+    HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask.data()));
+    HIP_CHECK(hipStreamSynchronize(streams_[kCompute]));
+    HIP_CHECK(hipStreamDestroy(streams_[kCompute]));
+    streams_[kCompute] = s;
+    reserved_ = n;
+  }
+  int reserved_cus() const override { return reserved_; }
   void* op_begin(StreamId s) override {
     if (!recording_) return streams_[s];
     HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
@@ -289,6 +305,7 @@ class HipBackend final : public Backend {
   }
 
   int dev_;
+  int reserved_ = 0;
   hipStream_t streams_[kNumStreams] = {nullptr, nullptr, nullptr};
   // graph recording state
   bool recording_ = false, in_op_ = false;

@@ -252,6 +252,15 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   nbuf_ = lag_ ? 3 : 2;
   if (const char* e = std::getenv("HEAT3D_FAKE_ALLREDUCE_US")) fake_allreduce_us_ = std::atof(e);
   chain_ = comm_->ordered_collectives() && !comm_->all_local() && comm_->size() > 1;
+  // CU reservation for the overlapped schedule of a real multi-rank job
+  // (RCCL or its phantom): the comm / boundary / check kernels must not queue
+  // behind the interior sweep, which holds every CU (LDS / VGPR file full)
+  {
+    int n = cfg_.reserve_cus;
+    if (const char* e = std::getenv("HEAT3D_RESERVE_CUS")) n = std::atoi(e);
+    if (n < 0) n = multi_stream() && !comm_->all_local() && comm_->size() > 1 ? 8 : 0;
+    if (be_->is_gpu() && n > 0) be_->reserve_cus(n);
+  }
 
   for (int r : comm_->local_ranks()) {
     Local l;
@@ -841,12 +850,16 @@ int Solver::long_sweeps_for(int64_t n) const {
 }
 
 bool Solver::graphs_allowed() const {
-  // Multi-stream (overlapped) schedules are graphs too (built explicitly by
-  // the backend's recorder); HEAT3D_GRAPH_MULTISTREAM=0 restricts graphs to
-  // the single-stream schedules.
+  // Multi-stream (overlapped) schedules can be graphs too (built explicitly by
+  // the backend's recorder, bitwise equal to eager runs: tests/test_gpu_graph.py),
+  // but only with HEAT3D_GRAPH_MULTISTREAM=1: the HIP runtime replays the
+  // graph's parallel branches without the comm stream's priority and without
+  // their overlap (phantom rank of the 8-GPU bench: 0.43 ms/step as a graph,
+  // 0.21 eager; profiles/rank_proxy_r02.md), so the overlapped schedule runs
+  // eagerly — its host cost is far below its GPU time at these sizes.
   static const bool ms_ok = [] {
     const char* e = std::getenv("HEAT3D_GRAPH_MULTISTREAM");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return cfg_.use_graph && be_->supports_graphs() && comm_->capturable() && !graph_failed_ && !phase_timing_ &&
          (!multi_stream() || ms_ok);

@@ -29,6 +29,8 @@ def main() -> int:
     ap.add_argument("--phantom", default="", help="R/P: run rank R of a P-rank job (PhantomComm)")
     args = ap.parse_args()
 
+    # multi-stream schedules are graphs only on request (solver.cpp graphs_allowed)
+    os.environ.setdefault("HEAT3D_GRAPH_MULTISTREAM", "1")
     import numpy as np
 
     import heat3d_amd

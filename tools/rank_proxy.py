@@ -66,6 +66,7 @@ def main() -> int:
     out = {"proxy": "phantom rank", "rank": r, "ranks": P, "dims": list(dims), "grid": args.grid,
            "dtype": args.dtype, "gbps": args.gbps, "ar_us": args.ar_us, "extra": args.extra,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "kernel": s.kernel,
+           "reserved_cus": s.native.reserved_cus, "graph_launches": s.native.graph_launches,
            "projected_node_glups": round(s.interior_points * args.steps / dt / 1e9, 2)}
     print(json.dumps(out), flush=True)
     return 0
