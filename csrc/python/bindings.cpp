@@ -640,6 +640,15 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("comm_transport_ranks", [](Solver& s) { return s.comm().transport_ranks(); })
       .def_property_readonly("device", [](Solver& s) { return s.backend().device(); })
       .def_property_readonly("reserved_cus", [](Solver& s) { return s.backend().reserved_cus(); })
+      .def_property_readonly("planned_bytes", &Solver::planned_bytes)
+      .def_property_readonly("mem_free_before", &Solver::mem_free_before)
+      .def_property_readonly("mem_total", &Solver::mem_total)
+      // (free, total) bytes of the backend's memory now (HBM: hipMemGetInfo)
+      .def("mem_info", [](Solver& s) -> py::tuple {
+        std::size_t f = 0, t = 0;
+        if (!s.backend().mem_info(&f, &t)) return py::make_tuple(py::none(), py::none());
+        return py::make_tuple(f, t);
+      })
       .def_property_readonly("kernel_name", &Solver::kernel_name)
       .def_property_readonly("temporal_blocking", &Solver::temporal_blocking)
       .def_property_readonly("temporal_steps", &Solver::temporal_steps)

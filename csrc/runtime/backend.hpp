@@ -34,6 +34,9 @@ class Backend {
   virtual void release(void* p) = 0;
   virtual void* alloc_host(std::size_t bytes) = 0;   // pinned host memory
   virtual void release_host(void* p) = 0;
+  // Free / total bytes of the memory alloc() draws from (device HBM; host
+  // RAM on the CPU backend).  false: unknown.
+  virtual bool mem_info(std::size_t* /*free*/, std::size_t* /*total*/) { return false; }
   virtual void copy(void* dst, const void* src, std::size_t bytes, CopyKind k, StreamId s) = 0;
   virtual void memset(void* dst, int v, std::size_t bytes, StreamId s) = 0;
 

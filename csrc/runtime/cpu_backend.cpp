@@ -1,8 +1,11 @@
 // heat3d-mi355x — CPU backend (OpenMP host kernels, synchronous execution).
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+
+#include <unistd.h>
 
 #include "backend.hpp"
 
@@ -26,6 +29,21 @@ class CpuBackend final : public Backend {
     return p;
   }
   void release(void* p) override { std::free(p); }
+  bool mem_info(std::size_t* free, std::size_t* total) override {
+    // MemAvailable (free + reclaimable page cache), not MemFree
+    const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
+    if (pages <= 0 || psz <= 0) return false;
+    *total = (std::size_t)pages * (std::size_t)psz;
+    std::FILE* fp = std::fopen("/proc/meminfo", "r");
+    if (!fp) return false;
+    char line[256];
+    bool found = false;
+    unsigned long long kb = 0;
+    while (!found && std::fgets(line, sizeof(line), fp)) found = std::sscanf(line, "MemAvailable: %llu kB", &kb) == 1;
+    std::fclose(fp);
+    *free = (std::size_t)kb * 1024;
+    return found;
+  }
   void* alloc_host(std::size_t bytes) override { return alloc(bytes); }
   void release_host(void* p) override { std::free(p); }
   void copy(void* dst, const void* src, std::size_t bytes, CopyKind, StreamId) override {

@@ -89,6 +89,10 @@ class HipBackend final : public Backend {
   bool is_gpu() const override { return true; }
   int device() const override { return dev_; }
 
+  bool mem_info(std::size_t* free, std::size_t* total) override {
+    HIP_CHECK(hipSetDevice(dev_));
+    return hipMemGetInfo(free, total) == hipSuccess;
+  }
   void* alloc(std::size_t bytes) override {
     void* p = nullptr;
     HIP_CHECK(hipMalloc(&p, bytes ? bytes : 256));

@@ -221,7 +221,6 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   int64_t min_n[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
   for (const auto& sd : dec_.subs)
     for (int a = 0; a < 3; ++a) min_n[a] = std::min(min_n[a], sd.n[a]);
-  const int64_t min_n0 = min_n[0];
   const bool block = dims[1] > 1 || dims[2] > 1;
   bool fits = true;
   for (int a = 0; a < 3; ++a) fits &= dims[a] == 1 || min_n[a] >= K;
@@ -261,6 +260,7 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     if (n < 0) n = multi_stream() && !comm_->all_local() && comm_->size() > 1 ? 8 : 0;
     if (be_->is_gpu() && n > 0) be_->reserve_cus(n);
   }
+  preflight_memory();
 
   for (int r : comm_->local_ranks()) {
     Local l;
@@ -341,6 +341,45 @@ Solver::~Solver() {
   be_->release(dstate_);
   be_->release_host(hstate_);
   comm_.reset();  // communicators before the device
+}
+
+// Refuses a configuration whose buffers do not fit before allocating any of
+// them: nbuf_ fields (with K-deep halos) per local rank plus the y / z face
+// staging buffers, against the backend's free memory less a reserve for RCCL
+// channels, code objects and scratch (HEAT3D_MEM_RESERVE_GB, default 2;
+// HEAT3D_MEM_PREFLIGHT=0 skips the check).  A 4096^3 fp32 grid on 2x2x2 GPUs
+// plans 3 x 34.6 GB per rank; 8192^3 fp32 on 2x2x2 (3 x 275 GB) is refused.
+void Solver::preflight_memory() {
+  planned_bytes_ = 0;
+  for (int r : comm_->local_ranks()) {
+    const Subdomain& sd = dec_.subs[r];
+    const Layout L = Layout::make(sd.n, (int64_t)esize_, hd_[0], hd_[1], hd_[2]);
+    planned_bytes_ += (std::size_t)nbuf_ * L.bytes();
+    if (comm_->all_local()) continue;
+    for (int a = 1; a < 3; ++a)  // packed y / z faces: a send and a receive buffer each
+      for (int side = 0; side < 2; ++side) {
+        if (!sd.has_neighbor(static_cast<Face>(2 * a + side))) continue;
+        std::size_t e = (std::size_t)hd_[a] * esize_;
+        for (int b = 0; b < 3; ++b)
+          if (b != a) e *= (std::size_t)(sd.n[b] + 2 * hd_[b]);
+        planned_bytes_ += 2 * e;
+      }
+  }
+  if (!be_->mem_info(&mem_free_before_, &mem_total_)) return;
+  const char* e = std::getenv("HEAT3D_MEM_PREFLIGHT");
+  if (e && e[0] == '0') return;
+  const char* rs = std::getenv("HEAT3D_MEM_RESERVE_GB");
+  const double reserve = (rs && *rs ? std::atof(rs) : 2.0) * 1e9;
+  if ((double)planned_bytes_ + reserve > (double)mem_free_before_) {
+    const auto& n = cfg_.n;
+    HEAT3D_THROW("memory preflight: the " << n[0] << "x" << n[1] << "x" << n[2] << " " << dtype_name(dt_)
+                 << " grid on " << comm_->size() << " rank(s) needs " << planned_bytes_ / 1e9 << " GB on this "
+                 << (be_->is_gpu() ? "GPU" : "host") << " (" << comm_->local_ranks().size() << " local subdomain(s) x "
+                 << nbuf_ << " field buffers + face staging) plus a " << reserve / 1e9 << " GB reserve, but only "
+                 << mem_free_before_ / 1e9 << " of " << mem_total_ / 1e9
+                 << " GB are free; use more ranks" << (dt_ == DType::F64 ? ", fp32" : "")
+                 << (nbuf_ == 3 ? ", or two field buffers (HEAT3D_LAG=0)" : ""));
+  }
 }
 
 bool Solver::is_root() const {

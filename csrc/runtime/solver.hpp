@@ -118,6 +118,12 @@ class Solver {
   int temporal_steps() const { return K_; }
   // field buffers per subdomain (3 = lagged convergence check of overlapped sweeps)
   int field_buffers() const { return nbuf_; }
+  // HBM preflight (constructor): bytes this solver allocates for its local
+  // ranks (fields + face staging), and the backend's free / total memory
+  // just before those allocations (0 when the backend cannot tell)
+  std::size_t planned_bytes() const { return planned_bytes_; }
+  std::size_t mem_free_before() const { return mem_free_before_; }
+  std::size_t mem_total() const { return mem_total_; }
 
   // Output / checkpoint.
   void write_tecplot(const std::string& path, const std::string& layout);
@@ -245,6 +251,8 @@ class Solver {
   // q+1 runs speculatively into the third buffer and only sweep q+2, which
   // overwrites sweep q's input (needed for a rollback), waits for it.
   int nbuf_ = 2;
+  std::size_t planned_bytes_ = 0, mem_free_before_ = 0, mem_total_ = 0;
+  void preflight_memory();
   bool lag_ = false;
   int64_t nsweep_ = 0;
   double fake_allreduce_us_ = 0;  // diagnostic: emulated all-reduce latency (virtual ranks)        // overlapped sweeps issued (event / residual-slot parity)

@@ -37,6 +37,42 @@ def test_golden_129_1e5_gpu(h3d, gpu):
     assert r["conv_iter"] == it and abs(r["error_percent"] - err) < 6e-5, r
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("eps", [1e-3, 1e-4, 1e-5])
+def test_goldens_257_gpu(h3d, gpu, eps):
+    """Convergence parity at the largest size the survey modelled (App. B.3;
+    91362 iterations at eps 1e-5)."""
+    it, err, norm = h3d.utils.golden(257, eps)
+    s, r = _solve(h3d, 257, eps)
+    assert r["converged"] and r["conv_iter"] == it, r
+    assert abs(r["error_percent"] - err) < 6e-5 and abs(r["norm"] - norm) < 1e-6, r
+
+
+@pytest.mark.slow
+def test_golden_257_slabs_gpu(h3d, gpu):
+    """Same golden through the 8-slab overlapped schedule (K-deep halos,
+    lagged check)."""
+    it, err, _ = h3d.utils.golden(257, 1e-3)
+    s, r = _solve(h3d, 257, 1e-3, virtual_ranks=8, decomp=(8, 1, 1))
+    assert r["conv_iter"] == it and abs(r["error_percent"] - err) < 6e-5, r
+
+
+def test_hbm_preflight(h3d, gpu):
+    """planned_bytes is what the solver takes from HBM (hipMemGetInfo before /
+    after), and a configuration that cannot fit is refused before allocating:
+    8192^3 fp32 on 2x2x2 GPUs needs 3 x 275 GB on each."""
+    s = h3d.HeatSolver((320, 320, 320), 10, 0.0, backend="hip", virtual_ranks=4, decomp=(4, 1, 1))
+    n = s.native
+    free_after, total = n.mem_info()
+    used = n.mem_free_before - free_after
+    assert total == n.mem_total and total > 250e9
+    assert n.planned_bytes <= used + (64 << 20) and used <= n.planned_bytes + (512 << 20), (used, n.planned_bytes)
+    with pytest.raises(Exception, match="memory preflight"):
+        h3d.HeatSolver((8192,) * 3, 10, 0.0, dtype="fp32", backend="hip", decomp=(2, 2, 2), phantom=(7, 8),
+                       device=0)
+    assert abs(n.mem_info()[0] - free_after) < (256 << 20)  # the refused solver allocated nothing
+
+
 def test_gpu_equals_cpu_bitwise(h3d, gpu):
     sg, rg = _solve(h3d, 41, 1e-4)
     sc, rc = _solve(h3d, 41, 1e-4, backend="cpu")

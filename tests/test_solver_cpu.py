@@ -239,3 +239,25 @@ def test_gather_refuses_oversized_grid(h3d, monkeypatch):
     monkeypatch.setenv("HEAT3D_HOST_MEM_LIMIT_GB", "0.0001")
     with pytest.raises(Exception, match="host memory"):
         s.gather()
+
+
+def test_memory_preflight(h3d, monkeypatch):
+    """Buffers are sized before any allocation: a configuration that does not
+    fit the backend's free memory is refused with the numbers (here host RAM;
+    HBM via hipMemGetInfo on the GPU backend, tests/test_gpu_solver.py)."""
+    s = h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu")
+    n = s.native
+    assert n.planned_bytes >= 2 * 42 ** 3 * 8 and n.mem_total > 0 and 0 < n.mem_free_before <= n.mem_total
+    free, total = n.mem_info()
+    assert total == n.mem_total and free > 0
+    # the phantom corner rank of 2x2x2 (K-deep y / z ghosts, packed face buffers)
+    p = h3d.HeatSolver((48, 48, 48), 5, 0.0, backend="cpu", decomp=(2, 2, 2), phantom=(7, 8),
+                       extra_args=["--temporal", "3"])
+    assert p.native.planned_bytes > p.native.field_buffers * 24 ** 3 * 8
+    with pytest.raises(Exception, match="memory preflight.*needs"):
+        h3d.HeatSolver((6000, 6000, 6000), 5, 0.0, backend="cpu")
+    monkeypatch.setenv("HEAT3D_MEM_RESERVE_GB", str(n.mem_free_before / 1e9))
+    with pytest.raises(Exception, match="memory preflight"):
+        h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu")
+    monkeypatch.setenv("HEAT3D_MEM_PREFLIGHT", "0")
+    h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu")

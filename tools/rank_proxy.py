@@ -51,10 +51,12 @@ def main() -> int:
     else:
         dims = tuple(int(v) for v in args.decomp.lower().split("x"))
     r = args.rank if args.rank >= 0 else min(1, P - 1)
+    gb = lambda b: None if b is None else round(b / 1e9, 2)
     s = HeatSolver(N, iter_max=1 << 40, eps=0.0, dtype=args.dtype, backend=args.backend, decomp=dims,
                    device=0 if args.backend == "hip" else None, phantom=(r, P),
                    extra_args=args.extra.split() if args.extra else ())
     s.initialize()
+    free_after, total = s.native.mem_info()
     s.step(args.warmup)
     s.synchronize()
     t0 = time.perf_counter()
@@ -67,7 +69,14 @@ def main() -> int:
            "dtype": args.dtype, "gbps": args.gbps, "ar_us": args.ar_us, "extra": args.extra,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "kernel": s.kernel,
            "reserved_cus": s.native.reserved_cus, "graph_launches": s.native.graph_launches,
-           "projected_node_glups": round(s.interior_points * args.steps / dt / 1e9, 2)}
+           "projected_node_glups": round(s.interior_points * args.steps / dt / 1e9, 2),
+           "rank_glups": round(s.interior_points / P * args.steps / dt / 1e9, 2),
+           "temporal_K": s.native.temporal_steps, "field_buffers": s.native.field_buffers,
+           # memory preflight (solver.cpp preflight_memory) and hipMemGetInfo
+           # before the solver's allocations / after initialize()
+           "mem_planned_gb": gb(s.native.planned_bytes), "mem_free_before_gb": gb(s.native.mem_free_before),
+           "mem_free_after_gb": gb(free_after), "mem_total_gb": gb(total),
+           "mem_used_gb": gb(s.native.mem_free_before - free_after) if free_after is not None else None}
     print(json.dumps(out), flush=True)
     return 0
 
