@@ -76,11 +76,18 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kComm], hipStreamNonBlocking, greatest));
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kReduce], hipStreamNonBlocking, greatest));
     HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
+    // per-stream capture streams (capture-to-graph recording) with the
+    // priorities of the streams they stand for
+    HIP_CHECK(hipStreamCreateWithPriority(&caps_[kCompute], hipStreamNonBlocking, least));
+    HIP_CHECK(hipStreamCreateWithPriority(&caps_[kComm], hipStreamNonBlocking, greatest));
+    HIP_CHECK(hipStreamCreateWithPriority(&caps_[kReduce], hipStreamNonBlocking, greatest));
   }
   ~HipBackend() override {
     (void)hipSetDevice(dev_);
     if (rec_) (void)hipGraphDestroy(rec_);
     if (cap_) (void)hipStreamDestroy(cap_);
+    for (auto& s : caps_)
+      if (s) (void)hipStreamDestroy(s);
     if (err_scratch_) (void)hipFree(err_scratch_);
     for (auto& s : streams_)
       if (s) (void)hipStreamDestroy(s);
@@ -118,9 +125,32 @@ class HipBackend final : public Backend {
       case CopyKind::D2D: kind = hipMemcpyDeviceToDevice; break;
       case CopyKind::H2H: kind = hipMemcpyHostToHost; break;
     }
+    if (recording_ && flatten_) {  // a memcpy node of the graph itself
+      HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
+      auto& t = tail_[s];
+      hipGraphNode_t node = nullptr;
+      HIP_CHECK(hipGraphAddMemcpyNode1D(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), dst, src, bytes, kind));
+      t.assign(1, node);
+      return;
+    }
     op(s, [&](hipStream_t st) { HIP_CHECK(hipMemcpyAsync(dst, src, bytes, kind, st)); });
   }
   void memset(void* dst, int v, std::size_t bytes, StreamId s) override {
+    if (recording_ && flatten_) {  // a memset node of the graph itself
+      HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
+      hipMemsetParams p{};
+      p.dst = dst;
+      p.elementSize = 1;
+      p.height = 1;
+      p.pitch = 0;
+      p.value = (unsigned)(v & 0xff);
+      p.width = bytes;
+      auto& t = tail_[s];
+      hipGraphNode_t node = nullptr;
+      HIP_CHECK(hipGraphAddMemsetNode(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), &p));
+      t.assign(1, node);
+      return;
+    }
     op(s, [&](hipStream_t st) { HIP_CHECK(hipMemsetAsync(dst, v, bytes, st)); });
   }
 
@@ -146,6 +176,13 @@ class HipBackend final : public Backend {
     HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
     in_op_ = true;
     op_s_ = s;
+    if (rmode_ == kToGraph) {
+      // capture straight into the recorded graph, behind the stream's frontier
+      auto& t = tail_[s];
+      HIP_CHECK(hipStreamBeginCaptureToGraph(caps_[s], rec_, t.empty() ? nullptr : t.data(), nullptr, t.size(),
+                                             hipStreamCaptureModeThreadLocal));
+      return caps_[s];
+    }
     HIP_CHECK(hipStreamBeginCapture(cap_, hipStreamCaptureModeThreadLocal));
     return cap_;
   }
@@ -154,13 +191,41 @@ class HipBackend final : public Backend {
     HEAT3D_CHECK(in_op_ && op_s_ == s, "graph recording: unbalanced operation");
     in_op_ = false;
     hipGraph_t g = nullptr;
+    if (rmode_ == kToGraph) {
+      // the new frontier: the capture's dependency set after the operation
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      const hipGraphNode_t* deps = nullptr;
+      std::size_t nd = 0;
+      hipError_t e = hipStreamGetCaptureInfo_v2(caps_[s], &cs, nullptr, nullptr, &deps, &nd);
+      std::vector<hipGraphNode_t> front(deps, deps + (e == hipSuccess ? nd : 0));
+      hipError_t e2 = hipStreamEndCapture(caps_[s], &g);
+      HIP_CHECK(e);
+      HIP_CHECK(e2);
+      if (!front.empty()) tail_[s] = std::move(front);
+      return;
+    }
     HIP_CHECK(hipStreamEndCapture(cap_, &g));
     std::size_t n = 0;
     hipError_t e = hipGraphGetNodes(g, nullptr, &n);
     if (e == hipSuccess && n > 0) {
       hipGraphNode_t node = nullptr;
       auto& t = tail_[s];
-      e = hipGraphAddChildGraphNode(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), g);
+      // a one-kernel operation becomes a kernel node of the graph itself (the
+      // runtime keeps a flat graph's independent branches on parallel
+      // streams); anything else (copies, multi-node captures) a child graph
+      bool flat = false;
+      if (n == 1 && flatten_) {
+        hipGraphNode_t only = nullptr;
+        hipGraphNodeType ty;
+        hipKernelNodeParams kp;
+        if (hipGraphGetNodes(g, &only, &n) == hipSuccess && hipGraphNodeGetType(only, &ty) == hipSuccess &&
+            ty == hipGraphNodeTypeKernel && hipGraphKernelNodeGetParams(only, &kp) == hipSuccess) {
+          e = hipGraphAddKernelNode(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), &kp);
+          flat = true;
+
+        }
+      }
+      if (!flat) e = hipGraphAddChildGraphNode(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), g);
       if (e == hipSuccess) t.assign(1, node);
     }
     (void)hipGraphDestroy(g);
@@ -222,17 +287,12 @@ class HipBackend final : public Backend {
   void* end_capture() override {
     HEAT3D_CHECK(recording_, "no graph recording active");
     recording_ = false;
-    if (in_op_) {  // an operation threw while being captured
-      in_op_ = false;
-      hipGraph_t g = nullptr;
-      (void)hipStreamEndCapture(cap_, &g);
-      if (g) (void)hipGraphDestroy(g);
-    }
+    if (in_op_) abort_op();  // an operation threw while being captured
     hipGraph_t g = rec_;
     rec_ = nullptr;
     evn_.clear();
     hipGraphExec_t ex = nullptr;
-    hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    hipError_t e = hipGraphInstantiateWithFlags(&ex, g, rmode_ == kToGraph ? hipGraphInstantiateFlagUseNodePriority : 0);
     (void)hipGraphDestroy(g);
     HIP_CHECK(e);
     return ex;
@@ -299,13 +359,22 @@ class HipBackend final : public Backend {
     try {
       f(st);
     } catch (...) {
-      in_op_ = false;
-      hipGraph_t g = nullptr;
-      (void)hipStreamEndCapture(cap_, &g);
-      if (g) (void)hipGraphDestroy(g);
+      abort_op();
       throw;
     }
     op_end(s);
+  }
+
+  void abort_op() {
+    in_op_ = false;
+    hipGraph_t g = nullptr;
+    if (rmode_ == kToGraph) {
+      (void)hipStreamEndCapture(caps_[op_s_], &g);  // g is rec_, owned by the recorder
+    } else {
+      (void)hipStreamEndCapture(cap_, &g);
+      if (g) (void)hipGraphDestroy(g);
+    }
+    (void)hipGetLastError();
   }
 
   int dev_;
@@ -317,6 +386,20 @@ class HipBackend final : public Backend {
   hipGraph_t rec_ = nullptr;
   hipStream_t cap_ = nullptr;                        // private one-operation capture stream
   std::vector<hipGraphNode_t> tail_[kNumStreams];    // dependency frontier per stream
+  hipStream_t caps_[kNumStreams] = {nullptr, nullptr, nullptr};
+  // how operations enter the recorded graph (HEAT3D_GRAPH_RECORD):
+  //   graph (default): captured straight into it (hipStreamBeginCaptureToGraph)
+  //   flat: captured alone, one-kernel captures re-added as kernel nodes,
+  //         copies / memsets added as nodes
+  //   child: every operation a child-graph node (HIP 7.2 replays those on the
+  //          launch stream only: no overlap, profiles/rank_proxy_r02.md)
+  enum RecordMode { kToGraph, kFlat, kChild };
+  const RecordMode rmode_ = [] {
+    const char* e = std::getenv("HEAT3D_GRAPH_RECORD");
+    const std::string v = e ? e : "";
+    return v == "child" ? kChild : v == "flat" ? kFlat : kToGraph;
+  }();
+  const bool flatten_ = rmode_ == kFlat;
   std::unordered_map<Event, std::vector<hipGraphNode_t>> evn_;  // event -> frontier at record
   double* err_scratch_ = nullptr;
   Roctx roctx_;

@@ -892,10 +892,11 @@ bool Solver::graphs_allowed() const {
   // Multi-stream (overlapped) schedules can be graphs too (built explicitly by
   // the backend's recorder, bitwise equal to eager runs: tests/test_gpu_graph.py),
   // but only with HEAT3D_GRAPH_MULTISTREAM=1: the HIP runtime replays the
-  // graph's parallel branches without the comm stream's priority and without
-  // their overlap (phantom rank of the 8-GPU bench: 0.43 ms/step as a graph,
-  // 0.21 eager; profiles/rank_proxy_r02.md), so the overlapped schedule runs
-  // eagerly — its host cost is far below its GPU time at these sizes.
+  // graph's parallel branches without stream priorities, so the boundary
+  // slabs and halo copies compete with the interior sweep (phantom rank of the
+  // 8-GPU bench: 0.28 ms/step as a graph, 0.21 eager; profiles/rank_proxy_r02.md)
+  // and the overlapped schedule runs eagerly — its host cost is far below its
+  // GPU time at these sizes.
   static const bool ms_ok = [] {
     const char* e = std::getenv("HEAT3D_GRAPH_MULTISTREAM");
     return e && e[0] == '1';
