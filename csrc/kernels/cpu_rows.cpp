@@ -25,7 +25,7 @@ static inline double row(const Real* __restrict in, Real* __restrict out, int64_
     const Real nv = ftcs_update<Real>(T, in[k - sx], in[k + sx], in[k - sy], in[k + sy], in[k - 1], in[k + 1], Dx,
                                       Dy, Dz);
     out[k] = nv;
-    const double d = std::fabs(static_cast<double>(nv) - static_cast<double>(T));
+    const double d = resid_abs(nv, T);  // in the field's precision (kernels.hpp)
     nan |= d != d;
     lres = d > lres ? d : lres;
   }

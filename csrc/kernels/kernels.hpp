@@ -86,6 +86,8 @@ void stencil_multi(DType t, const StencilParams& p, const KernelSpec& k, void* s
 void stencil_ring(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 // Same sweep, lean kernel (stencil_tbl.hip)
 void stencil_lean(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+// fp32 lean kernel on packed pairs of z columns (stencil_tbp.hip; spec tlK:2:…)
+void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream);
 // Any multi-step kind (TB2 / TBK / TBR / TBL) -> its kernel
 void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, void* stream);
@@ -156,6 +158,16 @@ H3D_HD inline Real ftcs_update(Real c, Real xm, Real xp, Real ym, Real yp, Real 
   const Real az = h3d_fma(Real(-2), c, zp) + zm;
   return h3d_fma(Dz, az, h3d_fma(Dy, ay, h3d_fma(Dx, ax, c)));
 }
+
+// Residual term of one point, |T^{n+1} - T^n|, taken in the field's
+// precision as the reference takes fabs(T - T0) in its field type
+// (heat3D.cu:1030-1033), then widened (exactly) to double for the max.  In
+// fp32 that is one subtraction instead of two conversions and a double
+// subtraction; in fp64 it is the same value as before.
+H3D_HD inline double resid_abs(double nv, double c) { return __builtin_fabs(nv - c); }
+H3D_HD inline double resid_abs(float nv, float c) { return (double)__builtin_fabsf(nv - c); }
+H3D_HD inline float resid_abs_r(float nv, float c) { return __builtin_fabsf(nv - c); }
+H3D_HD inline double resid_abs_r(double nv, double c) { return __builtin_fabs(nv - c); }
 
 H3D_HD inline void check_convergence_scalar(DeviceState* s, double r) {
   const int64_t t = s->iter;

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void stencil_naive(const Real* __restrict__ in
       const Real nv = ftcs<Real>(T, in[c - sx], in[c + sx], in[c - sy], in[c + sy], in[c - 1],
                                  in[c + 1], Dx, Dy, Dz);
       out[c] = nv;
-      m = res_max(m, fabs((double)nv - (double)T));
+      m = res_max(m, resid_abs(nv, T));
     }
   }
   if (res) residual_commit(res, m);
@@ -190,12 +190,12 @@ __global__ __launch_bounds__(256) void stencil_column(const Real* __restrict__ i
         Vec nv;
         if constexpr (V == 1) {
           nv = ftcs<Real>(c, qm[r], qp[r], ym, yp, zm, zp, Dx, Dy, Dz);
-          if (valid[0]) m = res_max(m, fabs((double)nv - (double)c));
+          if (valid[0]) m = res_max(m, resid_abs(nv, c));
         } else {
 #pragma unroll
           for (int v = 0; v < V; ++v) {
             nv[v] = ftcs<Real>(c[v], qm[r][v], qp[r][v], ym[v], yp[v], zm[v], zp[v], Dx, Dy, Dz);
-            if (valid[v]) m = res_max(m, fabs((double)nv[v] - (double)c[v]));
+            if (valid[v]) m = res_max(m, resid_abs(nv[v], c[v]));
           }
         }
         Real* dst = out + base0 + x * sx + (int64_t)r * sy;
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tile(const Real* __restr
 #pragma unroll
           for (int v = 0; v < V; ++v) {
             nv[v] = ftcs<Real>(c[v], qm[r][v], qp[r][v], ym[v], yp[v], zm[v], zp[v], Dx, Dy, Dz);
-            if (valid[v]) m = res_max(m, fabs((double)nv[v] - (double)c[v]));
+            if (valid[v]) m = res_max(m, resid_abs(nv[v], c[v]));
           }
           Real* dst = out + base0 + x * sx + (int64_t)r * sy;
           if (allvalid) {

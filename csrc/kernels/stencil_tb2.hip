@@ -187,7 +187,7 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tb2(const Real* __restri
           const Real nv = ftcs<Real>(c[v], qm[r][v], qp[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
           const bool in_box = yin && zin[v];
           u[v] = in_box ? nv : c[v];
-          if (in_box) m1 = res_max(m1, fabs((double)nv - (double)c[v]));
+          if (in_box) m1 = res_max(m1, resid_abs(nv, c[v]));
         }
         un[r] = u;
       }
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tb2(const Real* __restri
           const Real zm = v == 0 ? dpp_shr1(left, c[V - 1]) : c[v > 0 ? v - 1 : 0];
           const Real zp = v == V - 1 ? dpp_shl1(right, c[0]) : c[v + 1 < V ? v + 1 : 0];
           nv[v] = ftcs<Real>(c[v], um[r][v], un[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
-          if (rst && zst[v]) m2 = res_max(m2, fabs((double)nv[v] - (double)c[v]));
+          if (rst && zst[v]) m2 = res_max(m2, resid_abs(nv[v], c[v]));
         }
         if (rst) {
           Real* dst = out + base0 + (int64_t)xo * sx + (int64_t)r * sy;

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tbk(const Real* __restri
             const bool in_box = yin && zin[v];
             nr[v] = in_box ? nv : C[r][v];
             if (in_box && rval && cp[v] >= s && cp[v] < TZB - s)
-              m[s] = res_max(m[s], fabs((double)nv - (double)C[r][v]));
+              m[s] = res_max(m[s], resid_abs(nv, C[r][v]));
           }
           cpv<Real, V>(N[r], nr);
         }
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tbk(const Real* __restri
               const Real zm = v == 0 ? dpp_shr1(left, C[r][V - 1]) : C[r][v > 0 ? v - 1 : 0];
               const Real zp = v == V - 1 ? dpp_shl1(right, C[r][0]) : C[r][v + 1 < V ? v + 1 : 0];
               nv[v] = ftcs<Real>(C[r][v], M[r][v], P[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
-              if (rst && zst[v]) m[s] = res_max(m[s], fabs((double)nv[v] - (double)C[r][v]));
+              if (rst && zst[v]) m[s] = res_max(m[s], resid_abs(nv[v], C[r][v]));
             }
             if (rst) {
               Real* dst = out + base0 + (int64_t)p * sx + (int64_t)r * sy;

@@ -205,10 +205,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
 
   Real q[Q][R];              // T^n ring: plane p in slot (p - x0 + 1) mod Q
   Real f[K - 1][3][R];       // F_{s+1}(p) in f[s][(p + s) mod 3]
-  double m[K];               // per-lane residual maxima
+  Real m[K];                 // per-lane residual maxima (field precision, widened at the end)
   bool nan_seen = false;
 #pragma unroll
-  for (int s = 0; s < K; ++s) m[s] = 0.0;
+  for (int s = 0; s < K; ++s) m[s] = Real(0);
 #pragma unroll
   for (int s = 0; s < K - 1; ++s)
 #pragma unroll
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
         const Real zm = dpp_shr1z(C[r]);
         const Real zp = dpp_shl1z(C[r]);
         const Real nv = ftcs<Real>(C[r], M[r], P[r], ym, yp, zm, zp, Dx, Dy, Dz);
-        const double d = fabs((double)nv - (double)C[r]);
+        const Real d = resid_abs_r(nv, C[r]);
         bool upd = true, cnt = true, st = true;
         if constexpr (!FAST) {
           upd = xin && ((ybits >> r) & 1u);
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
       // widened by K-1-s (deep-halo points still in flight stay excluded)
       const bool ok = zin && lane >= s + 1 && lane < 63 - s && col >= g.blo[2] - (K - 1 - s) &&
                       col < g.bhi[2] + (K - 1 - s);
-      mm[s] = ok ? m[s] : 0.0;
+      mm[s] = ok ? (double)m[s] : 0.0;
     }
     // the row exchange buffer is dead: reuse it for the per-wave maxima
     __syncthreads();
@@ -400,6 +400,10 @@ template <typename Real>
 static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
   const KernelSpec r = k.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
   const int K = k.K, R = r.R, WY = r.WY, Q = r.NT;
+  if (sizeof(Real) == 4 && r.V == 2) {  // packed fp32 pairs (stencil_tbp.hip)
+    stencil_lean_pair(p, k, s);
+    return;
+  }
   HEAT3D_CHECK(r.V == 1 && r.WZ == 1, "tl kernels: one value per lane (V = 1), one wave across z (WZ = 1)");
 #define H3D_TBL(RR, YY, KK, QQ)                         \
   if (R == RR && WY == YY && K == KK && Q == QQ) {      \

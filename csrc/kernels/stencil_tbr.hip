@@ -231,13 +231,13 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
 #pragma unroll
         for (int v = 0; v < V; ++v) f[s][i][r][v] = Real(0);
 
-  double m[K][VA];
+  Real m[K][VA];  // residual maxima in the field's precision (widened at the end)
   bool nan_seen[VA];
 #pragma unroll
   for (int v = 0; v < VA; ++v) {
     nan_seen[v] = false;
 #pragma unroll
-    for (int s = 0; s < K; ++s) m[s][v] = 0.0;
+    for (int s = 0; s < K; ++s) m[s][v] = Real(0);
   }
   int par = 0;
 
@@ -315,9 +315,9 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
               const Real nv = ftcs<Real>(C[r][v], M[r][v], P[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
               N[r][v] = (yin && zin[v]) ? nv : C[r][v];
               if (rres) {
-                const double d = fabs((double)nv - (double)C[r][v]);
+                const Real d = resid_abs_r(nv, C[r][v]);
                 if constexpr (kColAcc) m[s][v < VA ? v : 0] = fmax(m[s][v < VA ? v : 0], d);
-                else m[s][0] = fmax(m[s][0], lres[kColAcc ? 0 : s][v] ? d : 0.0);
+                else m[s][0] = fmax(m[s][0], lres[kColAcc ? 0 : s][v] ? d : Real(0));
               }
             }
           }
@@ -337,12 +337,12 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
                 const Real zm = v > 0 ? C[r][v > 0 ? v - 1 : 0] : dpp_shr1z(C[r][V - 1]);
                 const Real zp = v < V - 1 ? C[r][v + 1 < V ? v + 1 : 0] : dpp_shl1z(C[r][0]);
                 nv[v] = ftcs<Real>(C[r][v], M[r][v], P[r][v], ym[v], yp[v], zm, zp, Dx, Dy, Dz);
-                const double d = fabs((double)nv[v] - (double)C[r][v]);
+                const Real d = resid_abs_r(nv[v], C[r][v]);
                 if constexpr (kColAcc) {
                   m[s][v < VA ? v : 0] = fmax(m[s][v < VA ? v : 0], d);
                   nan_seen[v < VA ? v : 0] |= nv[v] != nv[v];
                 } else {
-                  m[s][0] = fmax(m[s][0], zst[v] ? d : 0.0);
+                  m[s][0] = fmax(m[s][0], zst[v] ? d : Real(0));
                   nan_seen[0] |= zst[v] && nv[v] != nv[v];
                 }
               }
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbr(const Real* __restrict__ 
         const bool ok = !kColAcc || (s == K - 1 ? zst[v]
                                                 : (zin[v] && cp >= s && cp < TZ - s && kk >= g.blo[2] - (K - 1 - s) &&
                                                    kk < g.bhi[2] + (K - 1 - s)));
-        mm[s] = fmax(mm[s], ok ? m[s][v] : 0.0);
+        mm[s] = fmax(mm[s], ok ? (double)m[s][v] : 0.0);
       }
     }
     residual_commit_block<WY, K>(res, mm, nan_any, s_red);

@@ -75,12 +75,31 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kCompute], hipStreamNonBlocking, least));
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kComm], hipStreamNonBlocking, greatest));
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kReduce], hipStreamNonBlocking, greatest));
-    HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
-    // per-stream capture streams (capture-to-graph recording) with the
-    // priorities of the streams they stand for
-    HIP_CHECK(hipStreamCreateWithPriority(&caps_[kCompute], hipStreamNonBlocking, least));
-    HIP_CHECK(hipStreamCreateWithPriority(&caps_[kComm], hipStreamNonBlocking, greatest));
-    HIP_CHECK(hipStreamCreateWithPriority(&caps_[kReduce], hipStreamNonBlocking, greatest));
+    prio_[kCompute] = least;
+    prio_[kComm] = prio_[kReduce] = greatest;
+    // capture streams are created while a graph is recorded and destroyed
+    // after it: a process holds GPU_MAX_HW_QUEUES (4) hardware queues, and
+    // idle extra streams would make the comm stream share one with the
+    // interior sweep (2-rank RCCL on one GPU: 4.5 s -> 113 s)
+  }
+  hipStream_t capture_stream(StreamId s) {
+    if (!caps_[s]) HIP_CHECK(hipStreamCreateWithPriority(&caps_[s], hipStreamNonBlocking, prio_[s]));
+    return caps_[s];
+  }
+  hipStream_t child_capture_stream() {
+    if (!cap_) HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
+    return cap_;
+  }
+  void drop_capture_streams() {
+    for (auto& c : caps_)
+      if (c) {
+        (void)hipStreamDestroy(c);
+        c = nullptr;
+      }
+    if (cap_) {
+      (void)hipStreamDestroy(cap_);
+      cap_ = nullptr;
+    }
   }
   ~HipBackend() override {
     (void)hipSetDevice(dev_);
@@ -179,11 +198,11 @@ class HipBackend final : public Backend {
     if (rmode_ == kToGraph) {
       // capture straight into the recorded graph, behind the stream's frontier
       auto& t = tail_[s];
-      HIP_CHECK(hipStreamBeginCaptureToGraph(caps_[s], rec_, t.empty() ? nullptr : t.data(), nullptr, t.size(),
+      HIP_CHECK(hipStreamBeginCaptureToGraph(capture_stream(s), rec_, t.empty() ? nullptr : t.data(), nullptr, t.size(),
                                              hipStreamCaptureModeThreadLocal));
       return caps_[s];
     }
-    HIP_CHECK(hipStreamBeginCapture(cap_, hipStreamCaptureModeThreadLocal));
+    HIP_CHECK(hipStreamBeginCapture(child_capture_stream(), hipStreamCaptureModeThreadLocal));
     return cap_;
   }
   void op_end(StreamId s) override {
@@ -291,6 +310,7 @@ class HipBackend final : public Backend {
     hipGraph_t g = rec_;
     rec_ = nullptr;
     evn_.clear();
+    drop_capture_streams();
     hipGraphExec_t ex = nullptr;
     hipError_t e = hipGraphInstantiateWithFlags(&ex, g, rmode_ == kToGraph ? hipGraphInstantiateFlagUseNodePriority : 0);
     (void)hipGraphDestroy(g);
@@ -378,6 +398,7 @@ class HipBackend final : public Backend {
   }
 
   int dev_;
+  int prio_[kNumStreams] = {0, 0, 0};
   int reserved_ = 0;
   hipStream_t streams_[kNumStreams] = {nullptr, nullptr, nullptr};
   // graph recording state

@@ -145,8 +145,10 @@ KernelSpec KernelSpec::resolved(DType t) const {
     case TBL:  // lean kernel: 16 waves of 64 columns.  fp64: 3 rows per wave
                // (48-row tiles), 2 from K = 4 (32-row tiles: 115 VGPRs, no
                // spill); fp32: 4 rows from K = 4 (64-row tiles)
-      def(r.V, 1);
-      def(r.R, f64 ? (K >= 4 ? 2 : 3) : (K >= 4 && K <= 5 ? 4 : 3));
+      // fp32 up to K = 4: packed pairs (V = 2, stencil_tbp.hip: fp64's register
+      // shape, 1024^3 tl3:2:3 1450 vs tl4:1:4 1288 GLUPS on one box)
+      def(r.V, f64 || K > 4 ? 1 : 2);
+      def(r.R, (f64 || r.V == 2) ? (K >= 4 ? 2 : 3) : (K >= 4 && K <= 5 ? 4 : 3));
       def(r.WZ, 1);
       def(r.WY, 16);
       def(r.NT, 3);
@@ -212,7 +214,8 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
           : dt_ == DType::F64    ? kDefaultTemporal
                                  : kDefaultTemporalF32;
   // default kernel: the lean kernel (stencil_tbl.hip; MI355X 1024^3, same box:
-  // fp64 tl3 740-746 vs ring tr3 726-732 GLUPS, fp32 tl4 1168 vs tr3 1125),
+  // fp64 tl3 740-746 vs ring tr3 726-732 GLUPS; fp32 its packed-pair form
+  // stencil_tbp.hip, tl3:2:3 1450 vs tl4:1:4 1288),
   // except at K = 2 where the tuned queue kernel tb2 is used; tb2 / tbK /
   // trK / tlK force one
   if (!kspec2_.multi_step()) kspec2_.kind = K == 2 ? KernelSpec::TB2 : KernelSpec::TBL;

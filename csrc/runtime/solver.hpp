@@ -34,11 +34,12 @@ namespace heat3d {
 
 // Temporal blocking depth used when neither --temporal K nor --kernel2 tbK
 // names one: fp64 3 (the lean kernel is HBM-bound at K = 3; K = 4 does not
-// fit 16 waves x 128 VGPRs with 48-row tiles), fp32 4 (half the registers per
-// row: 64-row tiles; K = 5 is within 1% but needs 2K = 10 residual slots for
-// the lagged check of overlapped sweeps; profiles/kernel_sweep.md).
+// fit 16 waves x 128 VGPRs with 48-row tiles), fp32 3 (the packed-pair kernel,
+// two columns per lane, has fp64's register shape: 48 x 128 tiles; 1450 GLUPS
+// against 1288 for the one-column K = 4 kernel with 64-row tiles;
+// profiles/kernel_sweep.md).
 constexpr int kDefaultTemporal = 3;
-constexpr int kDefaultTemporalF32 = 4;
+constexpr int kDefaultTemporalF32 = 3;
 
 struct RunResult {
   bool converged = false;

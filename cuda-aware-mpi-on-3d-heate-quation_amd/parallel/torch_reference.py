@@ -108,7 +108,7 @@ class TorchReferenceSolver:
         for it in range(self.iter_max):
             self._exchange()
             new = ftcs_update(self.T, self.D)
-            res = (new.double() - self.T[1:-1, 1:-1, 1:-1].double()).abs().max().item()
+            res = (new - self.T[1:-1, 1:-1, 1:-1]).abs().max().double().item()  # field precision
             self.T[1:-1, 1:-1, 1:-1] = new
             r = self._allmax(max(res, 2.2250738585072014e-308))
             if it == 0 and r != 0.0:

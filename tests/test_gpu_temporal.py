@@ -111,8 +111,16 @@ VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16",
                   "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6"],
               2: ["tbk2", "tbk2:2:2:1:8", "tr2", "tr2:2:2:1:8:0:3", "tr2:1:4:1:16:0:3", "tr2:1:2:1:16",
                   "tl2", "tl2:1:2:1:16:0:3"]}
-VARIANTS_K_F32 = {3: ["tr3:2:4:1:8:0:3", "tr3:2:4:1:8:0:4", "tr3:2:4:1:16:0:3"], 4: ["tr4:2:4:1:8:0:4"],
-                  2: ["tr2:2:4:1:8:0:3", "tr2:2:4:1:8:0:4"]}
+# fp32 only: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)
+PAIR = {3: ["tl3:2:3:1:16:0:3", "tl3:2:3:1:16:0:4", "tl3:2:2:1:16:0:3", "tl3:2:3:1:16:5:3"],
+        4: ["tl4:2:2:1:16:0:3", "tl4:2:2:1:16:0:4", "tl4:2:2:1:16:7:3"],
+        2: ["tl2:2:2:1:16:0:3", "tl2:2:3:1:16:0:3"]}
+# round-1 ring-kernel variants that spill registers in fp32 since the residual
+# is taken in the field's precision (launch refuses them; tools/kres.sh)
+TBR_F32_SPILL = {"tr3:1:2:1:16:0:3", "tr3:2:4:1:8:0:4", "tr4:2:4:1:8:0:4", "tr3:2:4:1:16:0:3"}
+VARIANTS_K_F32 = {3: ["tr3:2:4:1:8:0:3"] + PAIR[3],
+                  4: PAIR[4],
+                  2: ["tr2:2:4:1:8:0:3"] + PAIR[2]}  # tr2:2:4:1:8:0:4 spills since the fp32 residual
 
 
 @pytest.mark.parametrize("K", [2, 3, 4])
@@ -131,6 +139,8 @@ def test_stencil_k_bitwise(h3d, gpu, K, dtype, n):
         refs.append(r)
     want = T[1:-1, 1:-1, 1:-1]
     for v in VARIANTS_K[K] + (VARIANTS_K_F32[K] if dtype == torch.float32 else []):
+        if dtype == torch.float32 and v in TBR_F32_SPILL:
+            continue
         out = ops.PaddedField(n, dtype=dtype, device=gpu)
         out.flat.fill_(-3.0)
         st = ops.new_state(gpu)
@@ -180,6 +190,18 @@ def _deep_random(ops, n, gx, dtype, seed):
 def test_sweep_deep_halo_matches_cpu(h3d, gpu, kernel, dtype, n0, box_x, side):
     """The slab path: K-plane ghost layers, u range widened into them, thin
     and partial x boxes.  gfx950 sweep == CPU K-single-steps definition."""
+    _deep_halo_case(h3d, gpu, kernel, dtype, n0, box_x, side)
+
+
+@pytest.mark.parametrize("kernel", PAIR[2] + PAIR[3] + PAIR[4])
+@pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (9, (0, 9), "hi"), (12, (4, 8), "both"),
+                                            (30, (0, 30), "both")])
+def test_sweep_pair_deep_halo_matches_cpu(h3d, gpu, kernel, n0, box_x, side):
+    """The packed fp32 pair kernel on the slab path."""
+    _deep_halo_case(h3d, gpu, kernel, torch.float32, n0, box_x, side)
+
+
+def _deep_halo_case(h3d, gpu, kernel, dtype, n0, box_x, side):
     ops = h3d.ops
     head = kernel.split(":")[0]
     K = 2 if head in ("tb2", "tbk2") else int(head[2])
@@ -239,6 +261,22 @@ def test_ring_kernel_solver_gpu(h3d, gpu, kernel2, vr):
     assert np.array_equal(a.gather(), b.gather())
 
 
+@pytest.mark.parametrize("kernel2,dtype", [("tl3:2:3:1:16:0:3", "fp32"), ("tl4:2:2:1:16:0:3", "fp32"),
+                                           ("tl2:2:2:1:16:0:3", "fp32")])
+@pytest.mark.parametrize("vr", [1, 3])
+def test_pair_kernel_solver_gpu(h3d, gpu, kernel2, dtype, vr):
+    """The packed fp32 kernel in the solver (single domain, x slabs):
+    bitwise equal to the CPU single-step solver, same convergence."""
+    n = (67, 45, 131)
+    a = h3d.HeatSolver(n, 10 ** 6, 1e-4, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=(vr, 1, 1),
+                       extra_args=["--kernel2", kernel2])
+    assert a.native.temporal_blocking and a.kernel.startswith(kernel2), a.kernel
+    b = h3d.HeatSolver(n, 10 ** 6, 1e-4, dtype=dtype, backend="cpu", extra_args=["--temporal", "1"])
+    ra, rb = a.run(), b.run()
+    assert ra["conv_iter"] == rb["conv_iter"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
 @pytest.mark.parametrize("kernel2", ["tr3", "tr2", "tb3", "tb2", "tl3", "tl4"])
 def test_sweep_nan_faults(h3d, gpu, kernel2):
     """A NaN anywhere in the field reaches the convergence check as a fault
@@ -255,7 +293,8 @@ def test_sweep_nan_faults(h3d, gpu, kernel2):
 @pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2), (2, 1, 3), (1, 3, 1), (1, 1, 2)])
 @pytest.mark.parametrize("kernel2,dtype", [("tr3", "fp64"), ("tr2", "fp64"), ("tr4", "fp64"),
                                            ("tr3:1:6:1:8:0:3", "fp64"), ("tr3", "fp32"), ("tr4:1:4:1:8:0:3", "fp32"),
-                                           ("tl3", "fp64"), ("tl4", "fp64"), ("tl4", "fp32")])
+                                           ("tl3", "fp64"), ("tl4", "fp64"), ("tl4", "fp32"),
+                                           ("tl3:2:3:1:16:0:3", "fp32"), ("tl4:2:2:1:16:0:3", "fp32")])
 def test_block_decomposition_ring_kernel_gpu(h3d, gpu, dims, kernel2, dtype):
     """Deep y / z halos (axis-ordered exchange with edges and corners) and the
     ring kernel's y / z update ranges: virtual-rank block decompositions on
@@ -304,6 +343,21 @@ def test_sweep_deep_yz_halo_matches_cpu(h3d, gpu, kernel, dtype, box, sides):
     y / z update ranges and its residual (only the box widened by K-1-s
     counts at stage s) equal the CPU K-single-steps definition on random
     fields, for thin / partial boxes such as the interior/boundary pieces."""
+    _deep_yz_case(h3d, gpu, kernel, dtype, box, sides)
+
+
+@pytest.mark.parametrize("kernel", ["tl3:2:3:1:16:0:3", "tl4:2:2:1:16:0:3", "tl2:2:2:1:16:0:3"])
+@pytest.mark.parametrize("box,sides", [((0, 12, 0, 50, 0, 140), "lo"), ((0, 12, 0, 50, 0, 140), "both"),
+                                       ((3, 9, 0, 4, 0, 140), "both"), ((0, 12, 46, 50, 5, 135), "both"),
+                                       ((0, 12, 0, 50, 136, 140), "both"), ((2, 10, 3, 47, 0, 4), "both"),
+                                       ((0, 12, 0, 50, 1, 139), "both"), ((0, 12, 0, 50, 3, 137), "hi")])
+def test_sweep_pair_deep_yz_halo_matches_cpu(h3d, gpu, kernel, box, sides):
+    """The packed fp32 pair kernel with y / z update ranges, odd and even box
+    starts along z (its tiles start on an even column)."""
+    _deep_yz_case(h3d, gpu, kernel, torch.float32, box, sides)
+
+
+def _deep_yz_case(h3d, gpu, kernel, dtype, box, sides):
     ops = h3d.ops
     head = kernel.split(":")[0]
     K = int(head[2])
