@@ -164,6 +164,8 @@ struct XPlan {
 // to chunks of U); cached per shape.  equal_only: no split (previous policy).
 XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_only = false);
 XPlan fixed_xplan(int64_t nx, int64_t tiles, int seg);
+// Makespan of a plan in the same greedy-dispatch model (plane steps per slot).
+double xplan_makespan(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fill, int U);
 
 }  // namespace hip
 }  // namespace heat3d

@@ -86,6 +86,8 @@ void stencil_multi(DType t, const StencilParams& p, const KernelSpec& k, void* s
 void stencil_ring(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 // Same sweep, lean kernel (stencil_tbl.hip)
 void stencil_lean(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+// z tile stride of the lean kernel for a box (host-side choice, stencil_tbl.hip)
+int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U, int L);
 // fp32 lean kernel on packed pairs of z columns (stencil_tbp.hip; spec tlK:2:…)
 void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream);
 // Any multi-step kind (TB2 / TBK / TBR / TBL) -> its kernel

@@ -488,6 +488,11 @@ static double simulate_xplan(const XPlan& p, int64_t nx, int64_t tiles, int slot
   return m;
 }
 
+double xplan_makespan(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fill, int U) {
+  std::vector<double> heap;
+  return simulate_xplan(p, nx, tiles, slots, fill, U, heap);
+}
+
 XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_only) {
   struct Key {
     int64_t nx, tiles;

@@ -54,6 +54,7 @@ struct TBLArgs {
   int c00, r00;                // first loaded column / row of tile (0, 0)
   int nzb, nyb;
   int segsplit, n1, rb;        // x plan (TBRArgs encoding)
+  int zs;                      // tile stride along z = stored columns per tile (<= 64 - 2K)
 };
 
 namespace {
@@ -107,7 +108,6 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
   // start of step x (Q-3 steps of cover)
   static_assert(Q == 3 || Q == 4 || Q == 6, "T^n ring size");
   constexpr int TY = WY * R;
-  constexpr int ZS = 64 - 2 * K;   // tile stride along z (stored columns)
   constexpr int YS = TY - 2 * K;   // tile stride along y (stored rows)
   // x-loop unroll making every ring index and the LDS parity static
   constexpr int U = lcm_l(lcm_l(Q, 3), 2);
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
 
   const int wave = sgpr(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int c0 = g.c00 + zb * ZS;           // tile's first loaded column
+  const int c0 = g.c00 + zb * g.zs;         // tile's first loaded column
   const int r0 = g.r00 + ybk * YS;          // tile's first loaded row
   const int yb = r0 + wave * R;             // this wave's first row
   const int col = c0 + lane;
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
 
   // per-lane masks (constant over the sweep)
   const bool zin = col >= g.uzlo && col < g.uzhi;
-  const bool zst = lane >= K && lane < 64 - K && col >= g.blo[2] && col < g.bhi[2];
+  const bool zst = lane >= K && lane < K + g.zs && col >= g.blo[2] && col < g.bhi[2];
 
   // ---- addressing: uniform base of row yb, column c0; clamped row offsets
   // (uniform by construction: kernel arguments and the readfirstlane'd wave
@@ -322,6 +322,37 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
   }
 }
 
+// Tile stride along z.  64 - 2K stored columns per 64-lane tile, or — fp64
+// only — the largest multiple of 8 below it, which starts every tile's stored
+// strip on a 64-byte boundary: whole 64-B write segments instead of partial
+// ones at both seams, worth 2-10% per sweep at equal tile counts (MI355X,
+// fp64 K = 3: 768^3 +2%, 1000^3 +3.5%, 1280^3 +10%; tools/gpu_zs2.sh).  The
+// narrower stride can add a tile column, so it is taken only where the
+// x-plan model, with that gain, predicts a shorter sweep (1024^3: 56 of 58,
+// +4.6%; 512^3 would cross a round of workgroups and keeps 58), and only for
+// boxes of >= 500 x planes: the slab shares of the 4- and 8-GPU runs (250 and
+// 122 interior planes) lost 13% and 8% with it in the phantom-rank proxy
+// while the 2-GPU share (510 planes) gained 1.5% (tools/gpu_zs3.sh).
+// HEAT3D_TL_ZS forces a stride.
+int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U, int L) {
+  const int wide = 64 - 2 * K;
+  static const int forced = [] {
+    const char* e = std::getenv("HEAT3D_TL_ZS");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  if (forced > 0 && forced <= wide) return forced;
+  const int aligned = esize == 8 ? wide & ~7 : wide;
+  if (aligned == wide || aligned <= 0 || nx < 500) return wide;
+  const int64_t nyb = std::max<int64_t>(1, (ny + TY - 2 * K - 1) / (TY - 2 * K));
+  auto cost = [&](int zs) {
+    const int64_t tiles = std::max<int64_t>(1, (nz + zs - 1) / zs) * nyb;
+    const XPlan p = L > 0 ? fixed_xplan(nx, tiles, L) : plan_x(nx, tiles, slots, 2 * (K - 1), U, L < 0);
+    return xplan_makespan(p, nx, tiles, slots, 2 * (K - 1), U);
+  };
+  constexpr double kAlignedGain = 0.92;
+  return cost(aligned) * kAlignedGain < cost(wide) ? aligned : wide;
+}
+
 template <typename Real, int R, int WY, int K, int Q>
 static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   const Box& b = p.box;
@@ -358,16 +389,18 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
                "tl: y/z update range outside the ghosted layout");
   HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live + 1 && g.ulo <= b.lo[0] && g.uhi >= b.hi[0],
                "tl: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
-  constexpr int ZS = 64 - 2 * K, YS = TY - 2 * K;
+  constexpr int YS = TY - 2 * K;
+  static const int slots =  // magic static: thread-safe under --gpus N
+      device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q>), 64 * WY);
+  constexpr int U = Q == 4 ? 12 : 6;  // the kernel's unroll (lcm(Q, 3, 2))
+  const int ZS = lean_z_stride(b.extent(0), b.extent(1), b.extent(2), K, (int)sizeof(Real), TY, slots, U, ks.L);
+  g.zs = ZS;
   g.c00 = (int)(b.lo[2] - K);
   g.r00 = (int)(b.lo[1] - K);
   g.nzb = (int)std::max<int64_t>(1, (b.extent(2) + ZS - 1) / ZS);
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
-  static const int slots =  // magic static: thread-safe under --gpus N
-      device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q>), 64 * WY);
   const int64_t ntiles = (int64_t)g.nzb * g.nyb;
   const int64_t nxb = b.extent(0);
-  constexpr int U = Q == 4 ? 12 : 6;  // the kernel's unroll (lcm(Q, 3, 2))
   XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
   HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
   g.segsplit = xp.seg | (xp.split << 16);

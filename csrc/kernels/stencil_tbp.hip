@@ -46,6 +46,7 @@ struct TBPArgs {
   int nzb, nyb;
   int segsplit, n1, rb;        // x plan (TBRArgs encoding)
   int hl;                      // first stored column of a tile, from its first loaded one
+  int zs;                      // tile stride along z = stored columns per tile (even, <= 128 - 2K - 2)
 };
 
 namespace {
@@ -98,7 +99,6 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
   static_assert(K >= 2 && K <= 6, "temporal depth");
   static_assert(Q == 3 || Q == 4, "T^n ring size");
   constexpr int TY = WY * R;
-  constexpr int ZS = 128 - 2 * K - 2;  // tile stride along z (stored columns)
   constexpr int YS = TY - 2 * K;       // tile stride along y (stored rows)
   constexpr int U = lcm_p(lcm_p(Q, 3), 2);
   static_assert(YS > 0 && R <= 16, "tile too small for depth K");
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
 
   const int wave = sgpr(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int c0 = g.c00 + zb * ZS;  // tile's first loaded column (even)
+  const int c0 = g.c00 + zb * g.zs;  // tile's first loaded column (even)
   const int r0 = g.r00 + ybk * YS;
   const int yb = r0 + wave * R;
   const int j0 = 2 * lane, j1 = j0 + 1;  // the pair's columns within the tile
@@ -167,8 +167,8 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
   static_assert(2 * R + K * R <= 32, "row mask bits");
 
   const bool zin0 = col0 >= g.uzlo && col0 < g.uzhi, zin1 = col1 >= g.uzlo && col1 < g.uzhi;
-  const bool zst0 = j0 >= g.hl && j0 < g.hl + ZS && col0 >= g.blo[2] && col0 < g.bhi[2];
-  const bool zst1 = j1 >= g.hl && j1 < g.hl + ZS && col1 >= g.blo[2] && col1 < g.bhi[2];
+  const bool zst0 = j0 >= g.hl && j0 < g.hl + g.zs && col0 >= g.blo[2] && col0 < g.bhi[2];
+  const bool zst1 = j1 >= g.hl && j1 < g.hl + g.zs && col1 >= g.blo[2] && col1 < g.bhi[2];
   const bool zst2 = zst0 && zst1;
 
   auto yclamp = [&](int row) { return min(max(row, g.ylo_live), g.yhi_live); };
@@ -344,7 +344,13 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
                "tl pair: y/z update range outside the ghosted layout");
   HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live + 1 && g.ulo <= b.lo[0] && g.uhi >= b.hi[0],
                "tl pair: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
-  constexpr int ZS = 128 - 2 * K - 2, YS = TY - 2 * K;
+  static const int zs_env = [] {
+    const char* e = std::getenv("HEAT3D_TP_ZS");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  const int ZS = zs_env > 0 && zs_env <= 128 - 2 * K - 2 && zs_env % 2 == 0 ? zs_env : 128 - 2 * K - 2;
+  g.zs = ZS;
+  constexpr int YS = TY - 2 * K;
   g.r00 = (int)(b.lo[1] - K);
   g.nzb = (int)std::max<int64_t>(1, (b.extent(2) + ZS - 1) / ZS);
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);

@@ -169,6 +169,10 @@ PYBIND11_MODULE(_heat3d, m) {
   py::register_exception<UsageError>(m, "UsageError", native_error.ptr());
 
   m.def("device_count", &hip_device_count);
+  // the lean kernel's z tile stride for a box (host model; tests/test_temporal_cpu.py)
+  m.def("lean_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U) {
+    return heat3d::hip::lean_z_stride(nx, ny, nz, K, esize, TY, slots, U, 0);
+  });
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
   // Which CUs a stream created with a CU mask reaches: runs the placement

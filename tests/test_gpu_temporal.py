@@ -405,3 +405,15 @@ def test_block_overlap_gpu(h3d, gpu, dims, dtype, monkeypatch):
     assert ra["last_residual"] == rb["last_residual"] == rc["last_residual"]
     ref = c.gather()
     assert np.array_equal(a.gather(), ref) and np.array_equal(b.gather(), ref)
+
+
+def test_aligned_z_stride_solver_gpu(h3d, gpu):
+    """A box thick enough for the 56-column (64-byte aligned) tile stride:
+    bitwise equal to the CPU single-step solver."""
+    n = (600, 40, 130)
+    assert h3d.native().lean_z_stride(598, 38, 128, 3, 8, 48, 256, 6) == 56
+    a = h3d.HeatSolver(n, 31, 0.0, backend="hip")
+    b = h3d.HeatSolver(n, 31, 0.0, backend="cpu", extra_args=["--temporal", "1"])
+    ra, rb = a.run(), b.run()
+    assert ra["iterations"] == rb["iterations"] == 31 and ra["last_residual"] == rb["last_residual"]
+    assert np.array_equal(a.gather(), b.gather())

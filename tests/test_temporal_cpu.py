@@ -262,3 +262,16 @@ def test_checkpoint_restart_across_temporal_decompositions(h3d, tmp_path, dims_a
     rb = b.run()
     assert rb["conv_iter"] == rf["conv_iter"]
     assert np.array_equal(b.gather(), full.gather())
+
+
+def test_lean_z_stride_model(h3d):
+    """fp64 lean-kernel tiles store 56 columns (64-byte aligned strips) instead
+    of 58 on thick boxes where the x-plan model predicts a shorter sweep, and
+    keep 58 on thin slabs and where a tile column would cross a round."""
+    n = h3d.native()
+    zs = lambda *b: n.lean_z_stride(*b, 3, 8, 48, 256, 6)  # noqa: E731
+    assert zs(1022, 1022, 1022) == 56 and zs(598, 38, 128) == 56
+    assert zs(510, 510, 510) == 58                      # 9 -> 10 tile columns crosses a round
+    assert zs(122, 1022, 1022) == 58 and zs(250, 1022, 1022) == 58  # 8- / 4-GPU slab shares
+    assert n.lean_z_stride(1022, 1022, 1022, 3, 4, 48, 256, 6) == 58  # fp32: unchanged
+    assert n.lean_z_stride(1022, 1022, 1022, 4, 8, 32, 256, 12) == 56  # 64 - 2K is aligned already
