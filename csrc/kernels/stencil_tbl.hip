@@ -54,7 +54,7 @@ struct TBLArgs {
   int c00, r00;                // first loaded column / row of tile (0, 0)
   int nzb, nyb;
   int segsplit, n1, rb;        // x plan (TBRArgs encoding)
-  int zs;                      // tile stride along z = stored columns per tile (<= 64 - 2K)
+  int zs;                      // tile stride along z = stored columns per tile (<= 64 - 2K) | tile order << 8
 };
 
 namespace {
@@ -78,13 +78,14 @@ __device__ __forceinline__ Real buf_load(__amdgpu_buffer_rsrc_t r, unsigned voff
   else
     return __builtin_bit_cast(Real, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
-template <typename Real>
+// AUX = cache policy bits of the store (2 = nt: streaming, not kept in L2)
+template <typename Real, int AUX = 0>
 __device__ __forceinline__ void buf_store(Real v, __amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
   if constexpr (sizeof(Real) == 8)
     __builtin_amdgcn_raw_buffer_store_b64(
-        __builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), v), r, voff, soff, 0);
+        __builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), v), r, voff, soff, AUX);
   else
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, AUX);
 }
 
 // f(integral_constant<int, I>) for I = B .. E-1, unrolled at compile time
@@ -98,7 +99,7 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 
 }  // namespace
 
-template <typename Real, int R, int WY, int K, int Q>
+template <typename Real, int R, int WY, int K, int Q, int NTS = 0>  // NTS: store cache policy
 __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ in, Real* __restrict__ out,
                                                        TBLArgs g, Real Dx, Real Dy, Real Dz,
                                                        unsigned long long* res, const int* done) {
@@ -135,10 +136,25 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     pc = g.n1 + remap(blk - g.n1 - rr, rr);
     part = 2;
   }
-  const int zb = pc % g.nzb;
-  const int tq = pc / g.nzb;
-  const int ybk = tq % g.nyb;
-  const int xs = tq / g.nyb;
+  // tile order inside an x segment: z fastest (py = 0), or z columns of py
+  // tile rows (bands), so that the workgroups an XCD runs at once form a
+  // compact patch whose shared halo rows / columns can hit its L2
+  const int zs = g.zs & 0xff, py = g.zs >> 8;
+  const int ntile = g.nzb * g.nyb;
+  const int xs = pc / ntile;
+  const int tt = pc - xs * ntile;
+  int zb, ybk;
+  if (py == 0) {
+    zb = tt % g.nzb;
+    ybk = tt / g.nzb;
+  } else {
+    const int band = tt / (g.nzb * py);
+    const int ylo = band * py;
+    const int pyb = min(py, g.nyb - ylo);
+    const int i = tt - band * g.nzb * py;
+    zb = i / pyb;
+    ybk = ylo + i % pyb;
+  }
   const int nxb = g.bhi[0] - g.blo[0];
   const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
   int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
@@ -147,7 +163,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
 
   const int wave = sgpr(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int c0 = g.c00 + zb * g.zs;         // tile's first loaded column
+  const int c0 = g.c00 + zb * zs;         // tile's first loaded column
   const int r0 = g.r00 + ybk * YS;          // tile's first loaded row
   const int yb = r0 + wave * R;             // this wave's first row
   const int col = c0 + lane;
@@ -166,24 +182,30 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
 
   // masked form, per row r (uniform, one SGPR): bit r = row in the update
   // range, bit R + r = stored row, bit 2R + s*R + r = row counted at stage s
-  unsigned ybits = 0;
+  // (64-bit when the rows x stages outgrow one SGPR: 8-wave tiles of 6 rows)
+  using YMask = std::conditional_t<(2 * R + K * R <= 32), unsigned, unsigned long long>;
+  static_assert(2 * R + K * R <= 64, "row mask bits");
+  YMask ybits = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int row = yb + r, rp = wave * R + r;
-    if (row >= g.uylo && row < g.uyhi) ybits |= 1u << r;
-    if (rp >= K && rp < TY - K && row >= g.blo[1] && row < g.bhi[1]) ybits |= 1u << (R + r);
+    if (row >= g.uylo && row < g.uyhi) ybits |= YMask(1) << r;
+    if (rp >= K && rp < TY - K && row >= g.blo[1] && row < g.bhi[1]) ybits |= YMask(1) << (R + r);
 #pragma unroll
     for (int s = 0; s < K; ++s)
       if (row >= g.uylo && row < g.uyhi && rp >= s + 1 && rp < TY - s - 1 && row >= g.blo[1] - (K - 1 - s) &&
           row < g.bhi[1] + (K - 1 - s))
-        ybits |= 1u << (2 * R + s * R + r);
+        ybits |= YMask(1) << (2 * R + s * R + r);
   }
-  ybits = (unsigned)sgpr((int)ybits);
-  static_assert(2 * R + K * R <= 32, "row mask bits");
+  if constexpr (sizeof(YMask) == 4) {
+    ybits = (unsigned)sgpr((int)ybits);
+  } else {
+    ybits = ((YMask)(unsigned)sgpr((int)(ybits >> 32)) << 32) | (unsigned)sgpr((int)(unsigned)ybits);
+  }
 
   // per-lane masks (constant over the sweep)
   const bool zin = col >= g.uzlo && col < g.uzhi;
-  const bool zst = lane >= K && lane < K + g.zs && col >= g.blo[2] && col < g.bhi[2];
+  const bool zst = lane >= K && lane < K + zs && col >= g.blo[2] && col < g.bhi[2];
 
   // ---- addressing: uniform base of row yb, column c0; clamped row offsets
   // (uniform by construction: kernel arguments and the readfirstlane'd wave
@@ -268,9 +290,9 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
         const Real d = resid_abs_r(nv, C[r]);
         bool upd = true, cnt = true, st = true;
         if constexpr (!FAST) {
-          upd = xin && ((ybits >> r) & 1u);
-          cnt = xcnt && ((ybits >> (2 * R + s * R + r)) & 1u);
-          st = xst && ((ybits >> (R + r)) & 1u);
+          upd = xin && ((ybits >> r) & 1);
+          cnt = xcnt && ((ybits >> (2 * R + s * R + r)) & 1);
+          st = xst && ((ybits >> (R + r)) & 1);
         }
         if (s < K - 1) {
           Real(&N)[R] = f[s < K - 1 ? s : 0][fw];
@@ -285,7 +307,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
         if (s == K - 1 && st) {
           // T^{n+K} on the stored region (inside the box, hence the update range)
           nan_seen |= zst && (nv != nv);
-          if (zst) buf_store<Real>(nv, plane_rsrc(outw + (int64_t)p * sx), lane_b, r * sy_b);
+          if (zst) buf_store<Real, NTS>(nv, plane_rsrc(outw + (int64_t)p * sx), lane_b, r * sy_b);
         }
       }
       if constexpr (Q == 3) {
@@ -353,7 +375,7 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
   return cost(aligned) * kAlignedGain < cost(wide) ? aligned : wide;
 }
 
-template <typename Real, int R, int WY, int K, int Q>
+template <typename Real, int R, int WY, int K, int Q, int NTS = 0>
 static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   const Box& b = p.box;
   constexpr int TY = WY * R;
@@ -391,10 +413,14 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
                "tl: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
   constexpr int YS = TY - 2 * K;
   static const int slots =  // magic static: thread-safe under --gpus N
-      device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q>), 64 * WY);
+      device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS>), 64 * WY);
   constexpr int U = Q == 4 ? 12 : 6;  // the kernel's unroll (lcm(Q, 3, 2))
   const int ZS = lean_z_stride(b.extent(0), b.extent(1), b.extent(2), K, (int)sizeof(Real), TY, slots, U, ks.L);
-  g.zs = ZS;
+  static const int order_py = [] {  // HEAT3D_TL_PY: tile rows per band of the tile order (0 = z fastest)
+    const char* e = std::getenv("HEAT3D_TL_PY");
+    return e && *e ? std::max(0, std::min(255, std::atoi(e))) : 0;
+  }();
+  g.zs = ZS | (std::min(order_py, 255) << 8);
   g.c00 = (int)(b.lo[2] - K);
   g.r00 = (int)(b.lo[1] - K);
   g.nzb = (int)std::max<int64_t>(1, (b.extent(2) + ZS - 1) / ZS);
@@ -414,7 +440,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl: residual slots " << p.slot << "+" << K);
   static const int spill = [] {
     hipFuncAttributes a{};
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q>)) == hipSuccess
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS>)) == hipSuccess
                ? (int)a.localSizeBytes
                : 0;
   }();
@@ -423,7 +449,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
                                                   << " B of registers per lane (HEAT3D_ALLOW_SPILL=1 overrides)");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
-  hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+  hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
                      static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0], (Real)p.D[1],
                      (Real)p.D[2], r, done);
   HIPK_CHECK(hipGetLastError());
@@ -438,17 +464,27 @@ static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_
     return;
   }
   HEAT3D_CHECK(r.V == 1 && r.WZ == 1, "tl kernels: one value per lane (V = 1), one wave across z (WZ = 1)");
-#define H3D_TBL(RR, YY, KK, QQ)                         \
-  if (R == RR && WY == YY && K == KK && Q == QQ) {      \
-    launch_tbl<Real, RR, YY, KK, QQ>(p, k, s);          \
-    return;                                             \
+#define H3D_TBL(RR, YY, KK, QQ)                                    \
+  if (R == RR && WY == YY && K == KK && Q == QQ && r.O <= 0) {     \
+    launch_tbl<Real, RR, YY, KK, QQ>(p, k, s);                     \
+    return;                                                        \
   }
+  // output-store cache-policy bits (spec field 7: 2 = nt, 1 / 16 = sc0 / sc1), default shape only
+#define H3D_TBLA(AA)                                                  \
+  if (R == 3 && WY == 16 && K == 3 && Q == 3 && r.O == (AA)) {        \
+    launch_tbl<Real, 3, 16, 3, 3, (AA)>(p, k, s);                     \
+    return;                                                           \
+  }
+  H3D_TBLA(2) H3D_TBLA(3) H3D_TBLA(17) H3D_TBLA(18) H3D_TBLA(19)
+#undef H3D_TBLA
   // 16 waves (<= 128 VGPRs, LDS 2K x 16 KiB): K <= 4; 12 waves (<= 168 VGPRs): K = 5
   H3D_TBL(3, 16, 4, 3) H3D_TBL(3, 16, 4, 4) H3D_TBL(3, 16, 3, 3) H3D_TBL(3, 16, 3, 4)
   H3D_TBL(2, 16, 4, 3) H3D_TBL(2, 16, 4, 4) H3D_TBL(2, 16, 5, 3) H3D_TBL(2, 16, 3, 3)
   H3D_TBL(2, 16, 4, 6) H3D_TBL(2, 16, 3, 6) H3D_TBL(3, 16, 3, 6) H3D_TBL(2, 16, 2, 6)
   H3D_TBL(3, 16, 2, 3) H3D_TBL(2, 16, 2, 3)
   H3D_TBL(4, 12, 4, 3) H3D_TBL(4, 12, 4, 4) H3D_TBL(4, 12, 5, 3) H3D_TBL(3, 12, 5, 3)
+  // 8 waves (<= 256 VGPRs, 2 per SIMD): 48-row tiles at K = 4
+  H3D_TBL(6, 8, 4, 3) H3D_TBL(6, 8, 3, 3) H3D_TBL(6, 8, 4, 4) H3D_TBL(5, 8, 4, 3)
   if constexpr (sizeof(Real) == 4) {
     // fp32: half the registers and LDS per row, so deeper sweeps fit 16 waves
     H3D_TBL(4, 16, 4, 3) H3D_TBL(3, 16, 5, 3) H3D_TBL(4, 16, 5, 3) H3D_TBL(3, 16, 6, 3)

@@ -64,12 +64,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t prs(const void* base) {
 __device__ __forceinline__ f2 ld2(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
   return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
+// AUX = cache-policy bits of the output stores (0 = default, 2 = nt)
+template <int AUX>
 __device__ __forceinline__ void st2(f2 v, __amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), v), r,
-                                        voff, soff, 0);
+                                        voff, soff, AUX);
 }
+template <int AUX>
 __device__ __forceinline__ void st1(float v, __amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, AUX);
 }
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
@@ -92,7 +95,7 @@ __device__ __forceinline__ void static_for_p(Fn&& fn) {
 
 }  // namespace
 
-template <int R, int WY, int K, int Q>
+template <int R, int WY, int K, int Q, int AUX = 0>
 __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__ in, float* __restrict__ out,
                                                        TBPArgs g, float Dxs, float Dys, float Dzs,
                                                        unsigned long long* res, const int* done) {
@@ -263,10 +266,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
           nan_seen |= (zst0 && nv.x != nv.x) || (zst1 && nv.y != nv.y);
           const __amdgpu_buffer_rsrc_t ro = prs(outw + (int64_t)p * sx);
           if (zst2) {
-            st2(nv, ro, lane_b, r * sy_b);
+            st2<AUX>(nv, ro, lane_b, r * sy_b);
           } else {
-            if (zst0) st1(nv.x, ro, lane_b, r * sy_b);
-            if (zst1) st1(nv.y, ro, lane_b + 4u, r * sy_b);
+            if (zst0) st1<AUX>(nv.x, ro, lane_b, r * sy_b);
+            if (zst1) st1<AUX>(nv.y, ro, lane_b + 4u, r * sy_b);
           }
         }
       }
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
   }
 }
 
-template <int R, int WY, int K, int Q>
+template <int R, int WY, int K, int Q, int AUX = 0>
 static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   const Box& b = p.box;
   constexpr int TY = WY * R;
@@ -355,7 +358,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.nzb = (int)std::max<int64_t>(1, (b.extent(2) + ZS - 1) / ZS);
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
   static const int slots =  // magic static: thread-safe under --gpus N
-      device_slots(reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q>), 64 * WY);
+      device_slots(reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q, AUX>), 64 * WY);
   const int64_t ntiles = (int64_t)g.nzb * g.nyb;
   const int64_t nxb = b.extent(0);
   constexpr int U = Q == 4 ? 12 : 6;
@@ -369,7 +372,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl pair: residual slots " << p.slot << "+" << K);
   static const int spill = [] {
     hipFuncAttributes a{};
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q>)) == hipSuccess
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q, AUX>)) == hipSuccess
                ? (int)a.localSizeBytes
                : 0;
   }();
@@ -378,7 +381,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
                                                        << " B of registers per lane (HEAT3D_ALLOW_SPILL=1 overrides)");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
-  hipLaunchKernelGGL((stencil_tbp<R, WY, K, Q>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+  hipLaunchKernelGGL((stencil_tbp<R, WY, K, Q, AUX>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
                      static_cast<const float*>(p.in), static_cast<float*>(p.out), g, (float)p.D[0], (float)p.D[1],
                      (float)p.D[2], r, done);
   HIPK_CHECK(hipGetLastError());
@@ -390,11 +393,19 @@ void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream
   const int K = k.K, R = r.R, WY = r.WY, Q = r.NT;
   HEAT3D_CHECK(r.V == 2 && r.WZ == 1, "tl pair kernel: two values per lane (V = 2), one wave across z");
   hipStream_t s = S(stream);
-#define H3D_TBP(RR, YY, KK, QQ)                     \
-  if (R == RR && WY == YY && K == KK && Q == QQ) {  \
-    launch_tbp<RR, YY, KK, QQ>(p, k, s);            \
-    return;                                         \
+#define H3D_TBP(RR, YY, KK, QQ)                                \
+  if (R == RR && WY == YY && K == KK && Q == QQ && r.O <= 0) {  \
+    launch_tbp<RR, YY, KK, QQ>(p, k, s);                       \
+    return;                                                    \
   }
+  // output-store cache policy (spec field 7), default shape only
+#define H3D_TBPA(AA)                                                       \
+  if (R == 3 && WY == 16 && K == 3 && Q == 3 && r.O == (AA)) {             \
+    launch_tbp<3, 16, 3, 3, (AA)>(p, k, s);                                \
+    return;                                                                \
+  }
+  H3D_TBPA(2) H3D_TBPA(3) H3D_TBPA(17) H3D_TBPA(19)
+#undef H3D_TBPA
   H3D_TBP(3, 16, 3, 3) H3D_TBP(3, 16, 3, 4) H3D_TBP(2, 16, 3, 3) H3D_TBP(2, 16, 4, 3) H3D_TBP(2, 16, 4, 4)
   H3D_TBP(3, 16, 4, 3) H3D_TBP(2, 16, 2, 3) H3D_TBP(3, 16, 2, 3)
 #undef H3D_TBP

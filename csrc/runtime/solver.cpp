@@ -92,7 +92,7 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     k.WY = at(4);
     k.L = at(5);
     k.NT = at(6);
-    if (k.kind == TBR && parts.size() > 7) k.O = at(7);  // 1 = non-temporal output stores
+    if ((k.kind == TBR || k.kind == TBL) && parts.size() > 7) k.O = at(7);  // tr: 1 = non-temporal output stores; tl: store cache-policy bits
   } else {
     throw UsageError("unknown kernel '" + s +
                      "' (auto | naive | column[:V[:R[:L[:O[:NT]]]]] | tile|tb2..tb6|tbk2|tr2..tr6|tl2..tl6"
@@ -170,7 +170,7 @@ std::string KernelSpec::str() const {
            : K == 2      ? std::string("tbk2:")
                          : "tb" + std::to_string(K) + ":")
        << V << ":" << R << ":" << WZ << ":" << WY << ":" << L << ":" << NT;
-    if (kind == TBR && O == 1) os << ":1";
+    if ((kind == TBR && O == 1) || (kind == TBL && O > 0)) os << ":" << O;
     return os.str();
   }
   std::ostringstream os;

@@ -106,13 +106,14 @@ def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
 VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb3:1:4:1:16", "tb3:1:6:1:8", "tb3:1:4:2:8", "tb3:1:4:1:8:3",
                   "tr3", "tr3:1:3:1:16:0:3", "tr3:1:4:1:8:0:4", "tr3:1:6:1:8:0:3", "tr3:1:4:1:8:5:3", "tr3:1:2:1:16:0:3",
                   "tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5:3", "tl3:1:3:1:16:0:6",
-                  "tl3:1:2:1:16:7:6"],
+                  "tl3:1:2:1:16:7:6", "tl3:1:6:1:8:0:3", "tl3:1:3:1:16:0:3:2", "tl3:1:3:1:16:0:3:19"],
               4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1", "tr4", "tr4:1:4:1:8:0:3", "tr4:1:4:1:8:0:4",
-                  "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6"],
+                  "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6",
+                  "tl4:1:6:1:8:0:3", "tl4:1:6:1:8:0:4", "tl4:1:5:1:8:0:3", "tl4:1:6:1:8:7:3"],
               2: ["tbk2", "tbk2:2:2:1:8", "tr2", "tr2:2:2:1:8:0:3", "tr2:1:4:1:16:0:3", "tr2:1:2:1:16",
                   "tl2", "tl2:1:2:1:16:0:3"]}
 # fp32 only: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)
-PAIR = {3: ["tl3:2:3:1:16:0:3", "tl3:2:3:1:16:0:4", "tl3:2:2:1:16:0:3", "tl3:2:3:1:16:5:3"],
+PAIR = {3: ["tl3:2:3:1:16:0:3", "tl3:2:3:1:16:0:3:2", "tl3:2:3:1:16:0:4", "tl3:2:2:1:16:0:3", "tl3:2:3:1:16:5:3"],
         4: ["tl4:2:2:1:16:0:3", "tl4:2:2:1:16:0:4", "tl4:2:2:1:16:7:3"],
         2: ["tl2:2:2:1:16:0:3", "tl2:2:3:1:16:0:3"]}
 # round-1 ring-kernel variants that spill registers in fp32 since the residual
@@ -182,7 +183,8 @@ def _deep_random(ops, n, gx, dtype, seed):
 
 @pytest.mark.parametrize("kernel", ["tb2", "tbk2", "tb3", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb4", "tb4:1:6:1:8",
                                     "tr2", "tr3", "tr3:1:3:1:16:0:3", "tr4", "tr2:2:2:1:8:0:3",
-                                    "tl2", "tl3", "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:0:6"])
+                                    "tl2", "tl3", "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:0:6",
+                                    "tl4:1:6:1:8:0:3", "tl3:1:6:1:8:0:3"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (5, (0, 5), "lo"), (9, (0, 9), "hi"),
                                             (12, (4, 8), "both"), (12, (0, 4), "both"), (12, (8, 12), "both"),
