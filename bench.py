@@ -196,6 +196,10 @@ def run_rank(args) -> int:
     s = make(0.0, 1 << 40)
     s.initialize()
     s.step(max(1, args.warmup))
+    # capture the graphs the timed steps replay (untimed) while the GPU still
+    # runs the warm-up, so that it does not idle (and clock down) between the
+    # warm-up and the timed steps
+    s.prepare_steps(args.steps)
     s.synchronize()
     # race detection before timing: every face sent by the warm-up exchange
     # must match, bit for bit, the ghost layer the neighbour received
@@ -204,7 +208,6 @@ def run_rank(args) -> int:
         print(f"bench.py: rank {rank}: {bad_faces} halo face(s) differ after warm-up", file=sys.stderr)
         return 3
     warm = s.native.iterations_issued
-    s.prepare_steps(args.steps)  # capture the graphs the timed steps replay (untimed)
     g0 = s.native.graph_launches
     barrier(group)
     torch.cuda.synchronize()

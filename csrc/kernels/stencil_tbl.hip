@@ -469,13 +469,14 @@ static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_
     launch_tbl<Real, RR, YY, KK, QQ>(p, k, s);                     \
     return;                                                        \
   }
-  // output-store cache-policy bits (spec field 7: 2 = nt, 1 / 16 = sc0 / sc1), default shape only
-#define H3D_TBLA(AA)                                                  \
-  if (R == 3 && WY == 16 && K == 3 && Q == 3 && r.O == (AA)) {        \
-    launch_tbl<Real, 3, 16, 3, 3, (AA)>(p, k, s);                     \
+  // output-store cache-policy bits (spec field 7: 2 = nt, 1 / 16 = sc0 / sc1), default shapes only
+#define H3D_TBLA(RR, KK, AA)                                          \
+  if (R == RR && WY == 16 && K == KK && Q == 3 && r.O == (AA)) {      \
+    launch_tbl<Real, RR, 16, KK, 3, (AA)>(p, k, s);                   \
     return;                                                           \
   }
-  H3D_TBLA(2) H3D_TBLA(3) H3D_TBLA(17) H3D_TBLA(18) H3D_TBLA(19)
+  H3D_TBLA(3, 3, 2) H3D_TBLA(3, 3, 3) H3D_TBLA(3, 3, 17) H3D_TBLA(3, 3, 18) H3D_TBLA(3, 3, 19)
+  H3D_TBLA(2, 4, 2)  // the K = 4 default (long sweeps)
 #undef H3D_TBLA
   // 16 waves (<= 128 VGPRs, LDS 2K x 16 KiB): K <= 4; 12 waves (<= 168 VGPRs): K = 5
   H3D_TBL(3, 16, 4, 3) H3D_TBL(3, 16, 4, 4) H3D_TBL(3, 16, 3, 3) H3D_TBL(3, 16, 3, 4)

@@ -315,6 +315,9 @@ class HipBackend final : public Backend {
     hipError_t e = hipGraphInstantiateWithFlags(&ex, g, rmode_ == kToGraph ? hipGraphInstantiateFlagUseNodePriority : 0);
     (void)hipGraphDestroy(g);
     HIP_CHECK(e);
+    // upload now (ordered on the compute stream) so that the first launch
+    // does not pay for it
+    HIP_CHECK(hipGraphUpload(ex, streams_[kCompute]));
     return ex;
   }
   void launch_graph(void* ex) override {

@@ -152,6 +152,15 @@ KernelSpec KernelSpec::resolved(DType t) const {
       def(r.WZ, 1);
       def(r.WY, 16);
       def(r.NT, 3);
+      // fp64 default shape: non-temporal output stores (the sweep's output is
+      // not re-read before the next sweep; streaming it past L2 keeps the
+      // input halo lines resident).  MI355X, 1024^3 kernel level: 756 -> 798
+      // GLUPS, 512^3 / 768^3 +2-2.5%; fp32 pair kernel unchanged (tools/gpu_nt.sh)
+      // (also K = 4, the long sweeps of step counts that are not multiples of
+      // 3: 5.45 -> 5.38 ms per 1024^3 sweep.  Not K = 2: its partial sweep went
+      // from 3.96 to 5.45 ms with nt stores; profiles/bench_r02_driver_gap.md)
+      if (f64 && r.O < 0 && r.V == 1 && r.WY == 16 && r.NT == 3 && ((K == 3 && r.R == 3) || (K == 4 && r.R == 2)))
+        r.O = 2;
       break;
     default:
       break;
