@@ -173,6 +173,11 @@ PYBIND11_MODULE(_heat3d, m) {
   m.def("lean_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U) {
     return heat3d::hip::lean_z_stride(nx, ny, nz, K, esize, TY, slots, U, 0);
   });
+  // a kernel spec with its per-dtype defaults filled in, as the solver
+  // launches it (tests/test_temporal_cpu.py)
+  m.def("kernel_spec_resolved", [](const std::string& spec, const std::string& dtype) {
+    return heat3d::KernelSpec::parse(spec).resolved(dtype == "fp32" ? heat3d::DType::F32 : heat3d::DType::F64).str();
+  });
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
   // Which CUs a stream created with a CU mask reaches: runs the placement

@@ -275,3 +275,17 @@ def test_lean_z_stride_model(h3d):
     assert zs(122, 1022, 1022) == 58 and zs(250, 1022, 1022) == 58  # 8- / 4-GPU slab shares
     assert n.lean_z_stride(1022, 1022, 1022, 3, 4, 48, 256, 6) == 58  # fp32: unchanged
     assert n.lean_z_stride(1022, 1022, 1022, 4, 8, 32, 256, 12) == 56  # 64 - 2K is aligned already
+
+
+def test_lean_store_policy_defaults(h3d):
+    """fp64 lean sweeps of the default K = 3 / 4 shapes store with the nt cache
+    policy (profiles/nt_stores_r02.md); K = 2, fp32 and explicit policies are
+    left as given."""
+    r = h3d.native().kernel_spec_resolved
+    assert r("tl3", "fp64") == "tl3:1:3:1:16:0:3:2"
+    assert r("tl4", "fp64") == "tl4:1:2:1:16:0:3:2"
+    assert r("tl2", "fp64") == "tl2:1:3:1:16:0:3"
+    assert r("tl3:1:3:1:16:0:3:0", "fp64") == "tl3:1:3:1:16:0:3"
+    assert r("tl3:1:3:1:16:0:3:19", "fp64") == "tl3:1:3:1:16:0:3:19"
+    assert r("tl3:1:2:1:16", "fp64") == "tl3:1:2:1:16:0:3"
+    assert r("tl3", "fp32") == "tl3:2:3:1:16:0:3"
