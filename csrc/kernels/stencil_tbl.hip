@@ -470,20 +470,21 @@ static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_
     return;                                                        \
   }
   // output-store cache-policy bits (spec field 7: 2 = nt, 1 / 16 = sc0 / sc1), default shapes only
-#define H3D_TBLA(RR, KK, AA)                                          \
-  if (R == RR && WY == 16 && K == KK && Q == 3 && r.O == (AA)) {      \
-    launch_tbl<Real, RR, 16, KK, 3, (AA)>(p, k, s);                   \
+#define H3D_TBLA(RR, YY, KK, AA)                                      \
+  if (R == RR && WY == YY && K == KK && Q == 3 && r.O == (AA)) {      \
+    launch_tbl<Real, RR, YY, KK, 3, (AA)>(p, k, s);                   \
     return;                                                           \
   }
-  H3D_TBLA(3, 3, 2) H3D_TBLA(3, 3, 3) H3D_TBLA(3, 3, 17) H3D_TBLA(3, 3, 18) H3D_TBLA(3, 3, 19)
-  H3D_TBLA(2, 4, 2)  // the K = 4 default (long sweeps)
+  H3D_TBLA(3, 16, 3, 2) H3D_TBLA(3, 16, 3, 3) H3D_TBLA(3, 16, 3, 17) H3D_TBLA(3, 16, 3, 18) H3D_TBLA(3, 16, 3, 19)
+  H3D_TBLA(2, 16, 4, 2)  // the K = 4 default (long sweeps)
+  H3D_TBLA(3, 12, 4, 2) H3D_TBLA(4, 12, 4, 2)  // 12-wave K = 4 tiles (36 / 48 rows)
 #undef H3D_TBLA
   // 16 waves (<= 128 VGPRs, LDS 2K x 16 KiB): K <= 4; 12 waves (<= 168 VGPRs): K = 5
   H3D_TBL(3, 16, 4, 3) H3D_TBL(3, 16, 4, 4) H3D_TBL(3, 16, 3, 3) H3D_TBL(3, 16, 3, 4)
   H3D_TBL(2, 16, 4, 3) H3D_TBL(2, 16, 4, 4) H3D_TBL(2, 16, 5, 3) H3D_TBL(2, 16, 3, 3)
   H3D_TBL(2, 16, 4, 6) H3D_TBL(2, 16, 3, 6) H3D_TBL(3, 16, 3, 6) H3D_TBL(2, 16, 2, 6)
   H3D_TBL(3, 16, 2, 3) H3D_TBL(2, 16, 2, 3)
-  H3D_TBL(4, 12, 4, 3) H3D_TBL(4, 12, 4, 4) H3D_TBL(4, 12, 5, 3) H3D_TBL(3, 12, 5, 3)
+  H3D_TBL(4, 12, 4, 3) H3D_TBL(4, 12, 4, 4) H3D_TBL(4, 12, 5, 3) H3D_TBL(3, 12, 5, 3) H3D_TBL(3, 12, 4, 3)
   // 8 waves (<= 256 VGPRs, 2 per SIMD): 48-row tiles at K = 4
   H3D_TBL(6, 8, 4, 3) H3D_TBL(6, 8, 3, 3) H3D_TBL(6, 8, 4, 4) H3D_TBL(5, 8, 4, 3)
   if constexpr (sizeof(Real) == 4) {

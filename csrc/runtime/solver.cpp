@@ -148,6 +148,13 @@ KernelSpec KernelSpec::resolved(DType t) const {
       // fp32 up to K = 4: packed pairs (V = 2, stencil_tbp.hip: fp64's register
       // shape, 1024^3 tl3:2:3 1450 vs tl4:1:4 1288 GLUPS on one box)
       def(r.V, f64 || K > 4 ? 1 : 2);
+      // fp64 K = 4 (the long sweeps of step counts that are not multiples of
+      // 3): 12 waves of 3 rows, 144 VGPRs, 750 vs 719 GLUPS for 16 x 2 rows
+      // with nt stores on one box (tools/gpu_k4.sh)
+      if (f64 && K == 4 && r.V == 1 && r.R == 0 && r.WY == 0) {
+        r.R = 3;
+        r.WY = 12;
+      }
       def(r.R, (f64 || r.V == 2) ? (K >= 4 ? 2 : 3) : (K >= 4 && K <= 5 ? 4 : 3));
       def(r.WZ, 1);
       def(r.WY, 16);
@@ -159,7 +166,9 @@ KernelSpec KernelSpec::resolved(DType t) const {
       // (also K = 4, the long sweeps of step counts that are not multiples of
       // 3: 5.45 -> 5.38 ms per 1024^3 sweep.  Not K = 2: its partial sweep went
       // from 3.96 to 5.45 ms with nt stores; profiles/bench_r02_driver_gap.md)
-      if (f64 && r.O < 0 && r.V == 1 && r.WY == 16 && r.NT == 3 && ((K == 3 && r.R == 3) || (K == 4 && r.R == 2)))
+      if (f64 && r.O < 0 && r.V == 1 && r.NT == 3 &&
+          ((K == 3 && r.R == 3 && r.WY == 16) || (K == 4 && r.R == 2 && r.WY == 16) ||
+           (K == 4 && r.R == 3 && r.WY == 12)))
         r.O = 2;
       break;
     default:

@@ -109,7 +109,8 @@ VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16",
                   "tl3:1:2:1:16:7:6", "tl3:1:6:1:8:0:3", "tl3:1:3:1:16:0:3:2", "tl3:1:3:1:16:0:3:19", "tl3:1:3:1:16:0:3:0"],
               4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1", "tr4", "tr4:1:4:1:8:0:3", "tr4:1:4:1:8:0:4",
                   "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6",
-                  "tl4:1:6:1:8:0:3", "tl4:1:6:1:8:0:4", "tl4:1:5:1:8:0:3", "tl4:1:6:1:8:7:3"],
+                  "tl4:1:6:1:8:0:3", "tl4:1:6:1:8:0:4", "tl4:1:5:1:8:0:3", "tl4:1:6:1:8:7:3",
+                  "tl4:1:3:1:12:0:3:2", "tl4:1:3:1:12:0:3"],
               2: ["tbk2", "tbk2:2:2:1:8", "tr2", "tr2:2:2:1:8:0:3", "tr2:1:4:1:16:0:3", "tr2:1:2:1:16",
                   "tl2", "tl2:1:2:1:16:0:3"]}
 # fp32 only: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)

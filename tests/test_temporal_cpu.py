@@ -283,7 +283,8 @@ def test_lean_store_policy_defaults(h3d):
     left as given."""
     r = h3d.native().kernel_spec_resolved
     assert r("tl3", "fp64") == "tl3:1:3:1:16:0:3:2"
-    assert r("tl4", "fp64") == "tl4:1:2:1:16:0:3:2"
+    assert r("tl4", "fp64") == "tl4:1:3:1:12:0:3:2"
+    assert r("tl4:1:2:1:16", "fp64") == "tl4:1:2:1:16:0:3:2"
     assert r("tl2", "fp64") == "tl2:1:3:1:16:0:3"
     assert r("tl3:1:3:1:16:0:3:0", "fp64") == "tl3:1:3:1:16:0:3"
     assert r("tl3:1:3:1:16:0:3:19", "fp64") == "tl3:1:3:1:16:0:3:19"
