@@ -52,6 +52,10 @@ struct StencilParams {
   int64_t ux[2] = {0, -1};
   // same for y and z (block decompositions with deep y / z halos)
   int64_t uy[2] = {0, -1}, uz[2] = {0, -1};
+  // multi-step kernels only: > 0 also updates the box shifted by xpair along
+  // x (the opposite boundary slab of an x slab), in the same launch where the
+  // kernel supports it (fp64 lean kernel), else as a second launch
+  int64_t xpair = 0;
 };
 
 struct InitParams {

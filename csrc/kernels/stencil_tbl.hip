@@ -157,8 +157,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
   }
   const int nxb = g.bhi[0] - g.blo[0];
   const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
-  int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
-  if (part == 1 && (g.rb >> 30)) xhi_p = min(xhi_p, xlo_p + split);
+  // rb < 0: paired x slabs, segment xs starts at xs * split (StencilParams::xpair)
+  const bool xpaired = g.rb < 0;
+  int xlo_p = xs * (xpaired ? split : seg), xhi_p = min(xlo_p + seg, nxb);
+  if (!xpaired && part == 1 && (g.rb >> 30)) xhi_p = min(xhi_p, xlo_p + split);
   if (part == 2) xlo_p = min(xlo_p + split, xhi_p);
 
   const int wave = sgpr(threadIdx.x >> 6);
@@ -376,37 +378,60 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
 }
 
 template <typename Real, int R, int WY, int K, int Q, int NTS = 0>
-static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
-  const Box& b = p.box;
+static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s, bool swap_xy = false) {
+  // paired x slabs: the kernel's box is their hull, the x plan has exactly
+  // the two slabs as segments (each piece's window reproduces its own slab's
+  // update, count and store ranges; tests/test_gpu_temporal.py -k xpair)
+  Box b = p.box;
+  const int64_t xpair = p.xpair;
+  HEAT3D_CHECK(!(xpair > 0 && swap_xy), "tl: paired slabs cannot march along y");
+  if (xpair > 0) {
+    HEAT3D_CHECK(xpair >= p.box.extent(0) && xpair < (1 << 15) && p.box.extent(0) < (1 << 15),
+                 "tl: paired x slabs overlap or are too far apart (" << xpair << ")");
+    b.hi[0] = p.box.lo[0] + xpair + p.box.extent(0);
+  }
   constexpr int TY = WY * R;
+  // swap_xy: march along y with x as the tile rows (thin x slabs: a tile of
+  // WY*R x-rows covers the slab and its K-deep halos, workgroups march the
+  // long y extent).  The kernel is axis-agnostic through its strides and
+  // ranges, so the swap is a relabelling of the arguments.
   const Layout& L = p.L;
-  HEAT3D_CHECK(L.n[0] + 2 * L.gx < (1LL << 30) && L.n[1] + 2 * L.gy < (1LL << 30) &&
-                   L.sy * (int64_t)sizeof(Real) * (R + 2 * L.gy + TY + 2 * K) < (1LL << 31),
+  const int64_t Lsx = swap_xy ? L.sy : L.sx, Lsy = swap_xy ? L.sx : L.sy;
+  const int64_t Ln0 = swap_xy ? L.n[1] : L.n[0], Ln1 = swap_xy ? L.n[0] : L.n[1];
+  const int64_t Lg0 = swap_xy ? L.gy : L.gx, Lg1 = swap_xy ? L.gx : L.gy;
+  const int64_t(&pux)[2] = swap_xy ? p.uy : p.ux;
+  const int64_t(&puy)[2] = swap_xy ? p.ux : p.uy;
+  if (swap_xy) {
+    std::swap(b.lo[0], b.lo[1]);
+    std::swap(b.hi[0], b.hi[1]);
+  }
+  HEAT3D_CHECK(Ln0 + 2 * Lg0 < (1LL << 30) && Ln1 + 2 * Lg1 < (1LL << 30) &&
+                   Lsy * (int64_t)sizeof(Real) * (R + 2 * Lg1 + TY + 2 * K) < (1LL << 31),
                "tl: extents exceed 32-bit tile coordinates");
   TBLArgs g;
-  g.sx = L.sx;
-  g.sy = L.sy;
+  g.sx = Lsx;
+  g.sy = Lsy;
   g.origin = L.origin;
   for (int a = 0; a < 3; ++a) {
     g.blo[a] = (int)b.lo[a];
     g.bhi[a] = (int)b.hi[a];
   }
-  g.ulo = (int)(p.ux[1] >= p.ux[0] ? p.ux[0] : b.lo[0]);
-  g.uhi = (int)(p.ux[1] >= p.ux[0] ? p.ux[1] : b.hi[0]);
-  const bool wy = p.uy[1] >= p.uy[0], wz = p.uz[1] >= p.uz[0];
-  g.uylo = (int)(wy ? p.uy[0] : b.lo[1]);
-  g.uyhi = (int)(wy ? p.uy[1] : b.hi[1]);
+  g.ulo = (int)(pux[1] >= pux[0] ? pux[0] : b.lo[0]);
+  g.uhi = (int)(pux[1] >= pux[0] ? pux[1] : b.hi[0]);
+  const bool wy = puy[1] >= puy[0], wz = p.uz[1] >= p.uz[0];
+  g.uylo = (int)(wy ? puy[0] : b.lo[1]);
+  g.uyhi = (int)(wy ? puy[1] : b.hi[1]);
   g.uzlo = (int)(wz ? p.uz[0] : b.lo[2]);
   g.uzhi = (int)(wz ? p.uz[1] : b.hi[2]);
-  g.xlo_live = (int)-L.gx;
-  g.xhi_live = (int)(L.n[0] + L.gx - 1);
-  g.ylo_live = (int)-L.gy;
-  g.yhi_live = (int)(L.n[1] + L.gy - 1);
+  g.xlo_live = (int)-Lg0;
+  g.xhi_live = (int)(Ln0 + Lg0 - 1);
+  g.ylo_live = (int)-Lg1;
+  g.yhi_live = (int)(Ln1 + Lg1 - 1);
   // every loaded column of every tile lies inside the row's allocation: the
   // row starts zoff >= 16 elements before k = 0 (tiles start K <= 6 columns
   // before the box) and the tail pad covers the last tile's overhang
   HEAT3D_CHECK(b.lo[2] - K >= -L.zoff, "tl: tile columns before the row start");
-  HEAT3D_CHECK(g.uylo - 1 >= -L.gy && g.uyhi <= L.n[1] + L.gy && g.uylo <= b.lo[1] && g.uyhi >= b.hi[1] &&
+  HEAT3D_CHECK(g.uylo - 1 >= -Lg1 && g.uyhi <= Ln1 + Lg1 && g.uylo <= b.lo[1] && g.uyhi >= b.hi[1] &&
                    g.uzlo - 1 >= -L.gz && g.uzhi <= L.n[2] + L.gz && g.uzlo <= b.lo[2] && g.uzhi >= b.hi[2],
                "tl: y/z update range outside the ghosted layout");
   HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live + 1 && g.ulo <= b.lo[0] && g.uhi >= b.hi[0],
@@ -427,11 +452,18 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
   const int64_t ntiles = (int64_t)g.nzb * g.nyb;
   const int64_t nxb = b.extent(0);
-  XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
+  XPlan xp;
+  if (xpair > 0) {
+    xp.seg = (int)p.box.extent(0);
+    xp.split = (int)xpair;
+    xp.n1 = (int)(2 * ntiles);
+  } else {
+    xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
+  }
   HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
   g.segsplit = xp.seg | (xp.split << 16);
   g.n1 = xp.n1;
-  g.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
+  g.rb = xpair > 0 ? (int)0x80000000u : xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
   const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
   HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
   if (std::getenv("HEAT3D_TRACE"))
@@ -459,8 +491,37 @@ template <typename Real>
 static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
   const KernelSpec r = k.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
   const int K = k.K, R = r.R, WY = r.WY, Q = r.NT;
+  // Thin x slabs (the K-plane boundary slabs of x-slab decompositions) with
+  // the default tile: 3-wave tiles of 9 x-rows marching along y
+  // (launch_tbl swap_xy) instead of 48-row tiles marching 3 planes plus a
+  // 4-plane pipeline fill along x.  Opt-in (HEAT3D_TL_SWAP=1) until the
+  // phantom-rank measurements decide.
+  static const bool swap_ok = [] {
+    const char* e = std::getenv("HEAT3D_TL_SWAP");
+    return e && e[0] == '1';
+  }();
+  // Only x-slab decompositions (no deep y / z halos: the update ranges in y
+  // and z are the box's): a block decomposition's x slab with deep z halos
+  // (2x1x3 virtual ranks, 45x61x150) gave a different residual on the GPU
+  // with the swap, not yet explained, so those keep the x-marching tiles.
+  const Box& bx = p.box;
+  auto within = [](const int64_t(&u)[2], int64_t lo, int64_t hi) { return u[1] < u[0] || (u[0] >= lo && u[1] <= hi); };
+  if (swap_ok && K == 3 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && p.xpair == 0 &&
+      bx.extent(0) > 0 && bx.extent(0) <= 2 * K && bx.extent(1) >= 16 * bx.extent(0) &&
+      within(p.uy, bx.lo[1], bx.hi[1]) && within(p.uz, bx.lo[2], bx.hi[2])) {
+    if constexpr (sizeof(Real) == 8) launch_tbl<Real, 3, 3, 3, 3, 2>(p, k, s, true);
+    else launch_tbl<Real, 3, 3, 3, 3, 0>(p, k, s, true);
+    return;
+  }
   if (sizeof(Real) == 4 && r.V == 2) {  // packed fp32 pairs (stencil_tbp.hip)
-    stencil_lean_pair(p, k, s);
+    StencilParams a = p;
+    a.xpair = 0;
+    stencil_lean_pair(a, k, s);
+    if (p.xpair > 0) {  // its x plan has no paired form: second launch
+      a.box.lo[0] += p.xpair;
+      a.box.hi[0] += p.xpair;
+      stencil_lean_pair(a, k, s);
+    }
     return;
   }
   HEAT3D_CHECK(r.V == 1 && r.WZ == 1, "tl kernels: one value per lane (V = 1), one wave across z (WZ = 1)");

@@ -519,6 +519,16 @@ void stencil_ring(DType t, const StencilParams& p, const KernelSpec& k, void* st
 }
 
 void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
+  if (p.xpair > 0 && k.kind != KernelSpec::TBL) {
+    // two x slabs, one launch each (only the lean kernel pairs them)
+    StencilParams a = p;
+    a.xpair = 0;
+    sweep(t, a, k, stream);
+    a.box.lo[0] += p.xpair;
+    a.box.hi[0] += p.xpair;
+    sweep(t, a, k, stream);
+    return;
+  }
   switch (k.kind) {
     case KernelSpec::TBR: stencil_ring(t, p, k, stream); break;
     case KernelSpec::TBL: stencil_lean(t, p, k, stream); break;

@@ -407,6 +407,22 @@ PYBIND11_MODULE(_heat3d, m) {
     if (!k.multi_step()) throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 / tr2..tr6 kernel");
     hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
   });
+  // the same on a pair of x slabs: box and box shifted by xpair along x
+  // (StencilParams::xpair: one launch for the fp64 lean kernel)
+  hk.def("stencil_sweep_xpair", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
+                                   int64_t gx, std::array<int64_t, 6> box, std::array<int64_t, 2> ux,
+                                   std::array<double, 3> D, int64_t state_ptr, int slot, const std::string& kernel,
+                                   int64_t xpair, int64_t stream) {
+    DType t = dt_of(dt);
+    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
+    p.L = to_layout(n, (int64_t)dtype_size(t), gx);
+    p.ux[0] = ux[0];
+    p.ux[1] = ux[1];
+    p.xpair = xpair;
+    KernelSpec k = KernelSpec::parse(kernel);
+    if (!k.multi_step()) throw UsageError("stencil_sweep_xpair needs a multi-step kernel");
+    hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
+  });
   // deep ghosts on every axis (block decompositions): g = (gx, gy, gz),
   // u = update ranges (ux0, ux1, uy0, uy1, uz0, uz1)
   hk.def("stencil_sweep3", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,

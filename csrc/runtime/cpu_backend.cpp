@@ -73,7 +73,16 @@ class CpuBackend final : public Backend {
   // scratch fields (same ghosts).  Step s updates the box widened by K-1-s
   // planes into [ux0, ux1) and accumulates into residual slot `slot + s`
   // (tb2: slots slot, slot ^ 1).
-  void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId) override {
+  void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId sid) override {
+    if (p.xpair > 0) {  // paired x slabs: one after the other
+      StencilParams a = p;
+      a.xpair = 0;
+      stencil2(t, a, k, sid);
+      a.box.lo[0] += p.xpair;
+      a.box.hi[0] += p.xpair;
+      stencil2(t, a, k, sid);
+      return;
+    }
     if (p.state && p.state->done) return;
     const int K = k.kind == KernelSpec::TB2 ? 2 : k.K;
     for (int i = 0; i < 2; ++i)

@@ -767,8 +767,19 @@ void Solver::enqueue_multi(int bi, int Kp) {
   ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
   ev_wait(kComm, EV_CHK + chk_prev);
   be_->range_push("boundary");
-  for (auto& l : local_)
-    for (const Box& b : l.tb_boundary) be_->stencil2(dt_, params(l, b), ks, kComm);
+  for (auto& l : local_) {
+    const auto& bs = l.tb_boundary;
+    std::size_t i = 0;
+    if (pair_x_slabs(bs)) {
+      // the two x slabs in one launch (StencilParams::xpair): one grid of
+      // workgroups instead of two rounds of short sweeps behind the interior
+      StencilParams sp = params(l, bs[0]);
+      sp.xpair = bs[1].lo[0] - bs[0].lo[0];
+      be_->stencil2(dt_, sp, ks, kComm);
+      i = 2;
+    }
+    for (; i < bs.size(); ++i) be_->stencil2(dt_, params(l, bs[i]), ks, kComm);
+  }
   be_->range_pop();
   ev_record(EV_BND + q, kComm);
   // [C] all residuals, all checks: now, or (lagged, ordered collectives) after
@@ -780,6 +791,22 @@ void Solver::enqueue_multi(int bi, int Kp) {
   pending_.Kp = Kp;
   if (!(lag_ && chain_)) flush_pending_reduce();
   ++nsweep_;
+}
+
+// The first two boundary pieces are the low and high x slabs of one shape
+// (both x faces have a neighbour): with HEAT3D_PAIR_SLABS=1 sweep them as a
+// pair (one launch of x-marching tiles).  Off by default: the phantom rank of
+// the 8-GPU bench ran 0.217 ms per step paired vs 0.213 as two launches, and
+// thin slabs now take the y-marching tiles (stencil_tbl.hip swap_xy).
+bool Solver::pair_x_slabs(const std::vector<Box>& bs) const {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT3D_PAIR_SLABS");
+    return e && e[0] == '1';
+  }();
+  if (!on || bs.size() < 2) return false;
+  const Box &a = bs[0], &b = bs[1];
+  return a.lo[1] == b.lo[1] && a.hi[1] == b.hi[1] && a.lo[2] == b.lo[2] && a.hi[2] == b.hi[2] &&
+         a.extent(0) == b.extent(0) && a.extent(0) > 0 && b.lo[0] >= a.hi[0];
 }
 
 void Solver::reduce_and_check(StreamId s, int slot0, int Kp) {

@@ -194,6 +194,7 @@ class Solver {
   void comm_token_signal(StreamId s);
   // all-reduce + check of one sweep (residual slots slot0 .. slot0+Kp-1)
   void reduce_and_check(StreamId s, int slot0, int Kp);
+  bool pair_x_slabs(const std::vector<Box>& bs) const;
   // lagged overlapped sweeps: the all-reduce of sweep q is issued after the
   // halo of sweep q+1 (see enqueue_multi); flush issues a pending one
   void flush_pending_reduce();

@@ -129,12 +129,21 @@ def ftcs_step2(src: PaddedField, dst: PaddedField, D: Sequence[float], kernel: s
 
 def sweep(src: PaddedField, dst: PaddedField, D: Sequence[float], box: Sequence[int],
           ux: Sequence[int] = (0, -1), kernel: str = "tb3", state: Optional[torch.Tensor] = None,
-          slot: int = 0) -> None:
+          slot: int = 0, xpair: int = 0) -> None:
     """One K-step sweep (K from ``kernel``: tb2, tbk2, tb3..tb6) on ``box``
     = (x0, x1, y0, y1, z0, z1) of a deep-ghost field, with the intermediate
     steps computed on the x range ``ux`` (the solver's x-slab schedule).
+    ``xpair`` > 0 also sweeps the box shifted by ``xpair`` along x (the two
+    boundary slabs of an x slab; one launch for the fp64 lean kernel).
     GPU tensors run the gfx950 kernel, CPU tensors the K-single-steps
     definition (csrc/kernels/kernels_cpu.cpp)."""
+    if xpair and src.device.type != "cuda":
+        sweep(src, dst, D, box, ux, kernel, state, slot)
+        b = list(box)
+        b[0] += xpair
+        b[1] += xpair
+        sweep(src, dst, D, b, ux, kernel, state, slot)
+        return
     if src.layout != dst.layout or src.dtype != dst.dtype or src.device != dst.device:
         raise ValueError("src and dst must share layout, dtype and device")
     sptr = 0
@@ -145,7 +154,10 @@ def sweep(src: PaddedField, dst: PaddedField, D: Sequence[float], box: Sequence[
     args = (src.dt, src.data_ptr(), dst.data_ptr(), list(src.n), src.gx, list(box), list(ux), list(D), sptr, slot,
             kernel)
     if src.device.type == "cuda":
-        native().hip.stencil_sweep(*args, _stream_ptr(src.flat))
+        if xpair:
+            native().hip.stencil_sweep_xpair(*args, xpair, _stream_ptr(src.flat))
+        else:
+            native().hip.stencil_sweep(*args, _stream_ptr(src.flat))
     else:
         native().cpu.stencil_sweep(*args)
 

@@ -204,11 +204,73 @@ def test_sweep_pair_deep_halo_matches_cpu(h3d, gpu, kernel, n0, box_x, side):
     _deep_halo_case(h3d, gpu, kernel, torch.float32, n0, box_x, side)
 
 
-def _deep_halo_case(h3d, gpu, kernel, dtype, n0, box_x, side):
+@pytest.mark.parametrize("kernel,dtype", [("tl3", torch.float64), ("tl4", torch.float64), ("tl2", torch.float64),
+                                          ("tl3:1:3:1:16:0:3:0", torch.float64), ("tl3", torch.float32),
+                                          ("tr3", torch.float64)])
+@pytest.mark.parametrize("n0,thick", [(30, 3), (9, 3), (6, 3), (130, 3), (12, 4)])
+def test_sweep_xpair_matches_cpu(h3d, gpu, kernel, dtype, n0, thick):
+    """Both boundary slabs of an x slab in one launch (StencilParams::xpair):
+    equal to the two slabs swept separately by the CPU definition, residuals
+    included."""
+    ops = h3d.ops
+    head = kernel.split(":")[0]
+    K = int(head[2])
+    if thick < K or 2 * thick > n0:
+        pytest.skip("slabs thinner than K or overlapping")
+    n = (n0, 37, 133)
+    ux = (-(K - 1), n0 + K - 1)
+    box = (0, thick, 0, n[1], 0, n[2])
+    xpair = n0 - thick
+    D = (0.06, 0.05, 0.04)
+    src = _deep_random(ops, n, K, dtype, 11)
+    want = ops.PaddedField(n, dtype=dtype, gx=K)
+    want.flat.fill_(-5.0)
+    st_c = ops.new_state("cpu")
+    ops.sweep(src, want, D, box, ux, kernel=kernel, state=st_c, xpair=xpair)
+    dsrc = ops.PaddedField(n, dtype=dtype, device=gpu, gx=K)
+    dsrc.flat.copy_(src.flat)
+    got = ops.PaddedField(n, dtype=dtype, device=gpu, gx=K)
+    got.flat.fill_(-5.0)
+    st_g = ops.new_state(gpu)
+    ops.sweep(dsrc, got, D, box, ux, kernel=kernel, state=st_g, xpair=xpair)
+    torch.cuda.synchronize()
+    g, w = got.owned().cpu(), want.owned()
+    for x0, x1 in ((0, thick), (xpair, n0)):
+        assert torch.equal(g[x0:x1], w[x0:x1]), f"{kernel} {n0} slab {x0}: max diff {(g[x0:x1] - w[x0:x1]).abs().max().item()}"
+    assert torch.equal(g[thick:xpair], torch.full_like(g[thick:xpair], -5.0)), "wrote between the slabs"
+    for s in range(K):
+        assert ops.residual_from_state(st_g, s) == ops.residual_from_state(st_c, s), (kernel, s)
+
+
+@pytest.mark.parametrize("kernel", ["tl3", "tl3:1:3:1:16:0:3"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("n0,box_x,side,ny", [(12, (0, 3), "both", 64), (12, (9, 12), "both", 64),
+                                               (6, (0, 3), "lo", 100), (9, (6, 9), "hi", 49),
+                                               (20, (0, 4), "both", 70), (8, (0, 6), "both", 130)])
+def test_sweep_thin_slab_y_marching(h3d, gpu, kernel, dtype, n0, box_x, side, ny):
+    """Thin x slabs with a long y extent take the y-marching tiles with
+    HEAT3D_TL_SWAP=1 (the default tl3 spec; the explicit shape stays
+    x-marching): both equal the CPU K-single-steps definition.  The switch is
+    read once per process, so this runs in a child process."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = (f"import sys; sys.path[:0] = [{root!r}, {here!r}]; import torch, heat3d_amd as h3d; "
+            f"from test_gpu_temporal import _deep_halo_case; "
+            f"_deep_halo_case(h3d, torch.device('cuda', 0), {kernel!r}, torch.{str(dtype).split('.')[-1]}, "
+            f"{n0}, {box_x!r}, {side!r}, {ny})")
+    env = dict(os.environ, HEAT3D_TL_SWAP="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def _deep_halo_case(h3d, gpu, kernel, dtype, n0, box_x, side, ny=37):
     ops = h3d.ops
     head = kernel.split(":")[0]
     K = 2 if head in ("tb2", "tbk2") else int(head[2])
-    n = (n0, 37, 133)
+    n = (n0, ny, 133)
     ux = (-(K - 1) if side in ("lo", "both") else 0, n0 + (K - 1 if side in ("hi", "both") else 0))
     box = (box_x[0], box_x[1], 0, n[1], 0, n[2])
     D = (0.06, 0.05, 0.04)
