@@ -99,7 +99,9 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 
 }  // namespace
 
-template <typename Real, int R, int WY, int K, int Q, int NTS = 0>  // NTS: store cache policy
+// NTS: store cache policy; SW: swapped axes (x planes are the tile rows, the
+// kernel marches y): the row neighbours are the x terms of the update
+template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
 __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ in, Real* __restrict__ out,
                                                        TBLArgs g, Real Dx, Real Dy, Real Dz,
                                                        unsigned long long* res, const int* done) {
@@ -288,7 +290,9 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
         const Real yp = r == R - 1 ? hi : C[r + 1 < R ? r + 1 : 0];
         const Real zm = dpp_shr1z(C[r]);
         const Real zp = dpp_shl1z(C[r]);
-        const Real nv = ftcs<Real>(C[r], M[r], P[r], ym, yp, zm, zp, Dx, Dy, Dz);
+        // same operation order as kernels.hpp ftcs_update in both frames
+        const Real nv = SW ? ftcs<Real>(C[r], ym, yp, M[r], P[r], zm, zp, Dx, Dy, Dz)
+                           : ftcs<Real>(C[r], M[r], P[r], ym, yp, zm, zp, Dx, Dy, Dz);
         const Real d = resid_abs_r(nv, C[r]);
         bool upd = true, cnt = true, st = true;
         if constexpr (!FAST) {
@@ -377,8 +381,9 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
   return cost(aligned) * kAlignedGain < cost(wide) ? aligned : wide;
 }
 
-template <typename Real, int R, int WY, int K, int Q, int NTS = 0>
-static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s, bool swap_xy = false) {
+template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
+static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
+  constexpr bool swap_xy = SW;
   // paired x slabs: the kernel's box is their hull, the x plan has exactly
   // the two slabs as segments (each piece's window reproduces its own slab's
   // update, count and store ranges; tests/test_gpu_temporal.py -k xpair)
@@ -438,7 +443,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
                "tl: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
   constexpr int YS = TY - 2 * K;
   static const int slots =  // magic static: thread-safe under --gpus N
-      device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS>), 64 * WY);
+      device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW>), 64 * WY);
   constexpr int U = Q == 4 ? 12 : 6;  // the kernel's unroll (lcm(Q, 3, 2))
   const int ZS = lean_z_stride(b.extent(0), b.extent(1), b.extent(2), K, (int)sizeof(Real), TY, slots, U, ks.L);
   static const int order_py = [] {  // HEAT3D_TL_PY: tile rows per band of the tile order (0 = z fastest)
@@ -472,7 +477,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl: residual slots " << p.slot << "+" << K);
   static const int spill = [] {
     hipFuncAttributes a{};
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS>)) == hipSuccess
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW>)) == hipSuccess
                ? (int)a.localSizeBytes
                : 0;
   }();
@@ -481,7 +486,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
                                                   << " B of registers per lane (HEAT3D_ALLOW_SPILL=1 overrides)");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
-  hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+  hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
                      static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0], (Real)p.D[1],
                      (Real)p.D[2], r, done);
   HIPK_CHECK(hipGetLastError());
@@ -494,23 +499,19 @@ static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_
   // Thin x slabs (the K-plane boundary slabs of x-slab decompositions) with
   // the default tile: 3-wave tiles of 9 x-rows marching along y
   // (launch_tbl swap_xy) instead of 48-row tiles marching 3 planes plus a
-  // 4-plane pipeline fill along x.  Opt-in (HEAT3D_TL_SWAP=1) until the
-  // phantom-rank measurements decide.
+  // 4-plane pipeline fill along x.  Phantom rank of the 1024^3 fp64 slab
+  // bench (64 GB/s emulated links): 8 ranks 0.2135 -> 0.2084 ms per step, 4
+  // ranks 0.379 -> 0.359, 2 ranks unchanged (tools/gpu_swap.sh).
+  // HEAT3D_TL_SWAP=0 turns it off.
   static const bool swap_ok = [] {
     const char* e = std::getenv("HEAT3D_TL_SWAP");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
-  // Only x-slab decompositions (no deep y / z halos: the update ranges in y
-  // and z are the box's): a block decomposition's x slab with deep z halos
-  // (2x1x3 virtual ranks, 45x61x150) gave a different residual on the GPU
-  // with the swap, not yet explained, so those keep the x-marching tiles.
   const Box& bx = p.box;
-  auto within = [](const int64_t(&u)[2], int64_t lo, int64_t hi) { return u[1] < u[0] || (u[0] >= lo && u[1] <= hi); };
   if (swap_ok && K == 3 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && p.xpair == 0 &&
-      bx.extent(0) > 0 && bx.extent(0) <= 2 * K && bx.extent(1) >= 16 * bx.extent(0) &&
-      within(p.uy, bx.lo[1], bx.hi[1]) && within(p.uz, bx.lo[2], bx.hi[2])) {
-    if constexpr (sizeof(Real) == 8) launch_tbl<Real, 3, 3, 3, 3, 2>(p, k, s, true);
-    else launch_tbl<Real, 3, 3, 3, 3, 0>(p, k, s, true);
+      bx.extent(0) > 0 && bx.extent(0) <= 2 * K && bx.extent(1) >= 16 * bx.extent(0)) {
+    if constexpr (sizeof(Real) == 8) launch_tbl<Real, 3, 3, 3, 3, 2, true>(p, k, s);
+    else launch_tbl<Real, 3, 3, 3, 3, 0, true>(p, k, s);
     return;
   }
   if (sizeof(Real) == 4 && r.V == 2) {  // packed fp32 pairs (stencil_tbp.hip)
