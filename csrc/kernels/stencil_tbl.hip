@@ -514,6 +514,23 @@ static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_
     else launch_tbl<Real, 3, 3, 3, 3, 0, true>(p, k, s);
     return;
   }
+  // Medium x boxes (the interior of a thin slab share) with the default fp64
+  // tile: HEAT3D_TL_SWAP_X = N marches y when x <= N planes and y >= 4x.  A
+  // probe, off by default: one round of long y pieces instead of two rounds
+  // of x pieces lost on the phantom rank (8 ranks 0.2087 -> 0.2395 ms per
+  // step, 4 ranks 0.382 -> 0.475: 48-row bands over 122 / 250 x planes waste
+  // a third of a band, tools/gpu_swapx.sh).
+  static const int swap_x = [] {
+    const char* e = std::getenv("HEAT3D_TL_SWAP_X");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  if constexpr (sizeof(Real) == 8) {
+    if (swap_x > 0 && K == 3 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && p.xpair == 0 &&
+        bx.extent(0) <= swap_x && bx.extent(1) >= 4 * bx.extent(0)) {
+      launch_tbl<Real, 3, 16, 3, 3, 2, true>(p, k, s);
+      return;
+    }
+  }
   if (sizeof(Real) == 4 && r.V == 2) {  // packed fp32 pairs (stencil_tbp.hip)
     StencilParams a = p;
     a.xpair = 0;
