@@ -281,6 +281,12 @@ def run_rank(args) -> int:
         # the real HBM traffic is about 1/K of it with K-step temporal blocking
         "single_step_equiv_tbps_per_gpu": round(value / world * 2 * esize / 1e3, 3),
         "vs_single_step_roofline": round(value / roofline_glups(esize, world), 4),
+        # K-step roofline: one read + one write of the field per K steps (no
+        # tile overlap) at the float4-copy rate measured on these boxes
+        # (5.6 TB/s, profiles/hbm_probes_r02.md); the fp64 sweep's measured
+        # traffic is 19.1 B per point per 3 steps (profiles/pmc_tl3_nt_r02.md)
+        "temporal_roofline_glups_per_gpu": round(5.6e12 / (2 * esize / max(1, K)) / 1e9, 1),
+        "vs_temporal_roofline": round(value / world / (5.6e12 / (2 * esize / max(1, K)) / 1e9), 4),
         "time_to_converge": ttc,
         "baseline_note": "reference publishes no numbers (BASELINE.md); single-step roofline = "
                          "6.29 TB/s / (2*esize) per GPU",
