@@ -193,26 +193,41 @@ def run_rank(args) -> int:
                           device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
                           extra_args=["--temporal", str(args.temporal), "--kernel2", args.kernel2])
 
+    phase_log = os.environ.get("HEAT3D_BENCH_PHASES") == "1"
+    tp = [time.perf_counter()]
+
+    def phase(name):
+        if phase_log:
+            tp.append(time.perf_counter())
+            print(f"bench.py phase {name}: {1e3 * (tp[-1] - tp[-2]):.2f} ms", file=sys.stderr, flush=True)
+
     s = make(0.0, 1 << 40)
     s.initialize()
+    phase("initialize")
     s.step(max(1, args.warmup))
+    phase("warmup enqueued")
     # capture the graphs the timed steps replay (untimed) while the GPU still
     # runs the warm-up, so that it does not idle (and clock down) between the
     # warm-up and the timed steps
     s.prepare_steps(args.steps)
+    phase("graphs prepared")
     s.synchronize()
+    phase("warmup synchronized")
     # race detection before timing: every face sent by the warm-up exchange
     # must match, bit for bit, the ghost layer the neighbour received
     bad_faces = s.native.verify_halos()
     if bad_faces:
         print(f"bench.py: rank {rank}: {bad_faces} halo face(s) differ after warm-up", file=sys.stderr)
         return 3
+    phase("halos verified")
     warm = s.native.iterations_issued
     g0 = s.native.graph_launches
     barrier(group)
     torch.cuda.synchronize()
+    phase("barrier")
     t0 = time.perf_counter()
     s.step(args.steps)
+    phase("timed steps enqueued")
     s.synchronize()
     torch.cuda.synchronize()
     barrier(group)
