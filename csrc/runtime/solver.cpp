@@ -766,6 +766,13 @@ void Solver::enqueue_multi(int bi, int Kp) {
   flush_pending_reduce();
   ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
   ev_wait(kComm, EV_CHK + chk_prev);
+  // HEAT3D_BND_AFTER_INT=1: boundary slabs only after this sweep's interior
+  // (probe: with fast links they otherwise start mid-interior and take its CUs)
+  static const bool bnd_after_int = [] {
+    const char* e = std::getenv("HEAT3D_BND_AFTER_INT");
+    return e && e[0] == '1';
+  }();
+  if (bnd_after_int) ev_wait(kComm, EV_INT + q);
   be_->range_push("boundary");
   for (auto& l : local_) {
     const auto& bs = l.tb_boundary;
