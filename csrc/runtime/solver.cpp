@@ -166,6 +166,9 @@ KernelSpec KernelSpec::resolved(DType t) const {
       // (also K = 4, the long sweeps of step counts that are not multiples of
       // 3: 5.45 -> 5.38 ms per 1024^3 sweep.  Not K = 2: its partial sweep went
       // from 3.96 to 5.45 ms with nt stores; profiles/bench_r02_driver_gap.md)
+      // fp32 packed-pair default shape too: 1388 -> 1431 GLUPS at 1024^3, 1354
+      // -> 1513 at 2049^3 (tools/gpu_tpzs.sh)
+      if (!f64 && r.O < 0 && r.V == 2 && K == 3 && r.R == 3 && r.WY == 16 && r.NT == 3) r.O = 2;
       if (f64 && r.O < 0 && r.V == 1 && r.NT == 3 &&
           ((K == 3 && r.R == 3 && r.WY == 16) || (K == 4 && r.R == 2 && r.WY == 16) ||
            (K == 4 && r.R == 3 && r.WY == 12)))

@@ -278,9 +278,9 @@ def test_lean_z_stride_model(h3d):
 
 
 def test_lean_store_policy_defaults(h3d):
-    """fp64 lean sweeps of the default K = 3 / 4 shapes store with the nt cache
-    policy (profiles/nt_stores_r02.md); K = 2, fp32 and explicit policies are
-    left as given."""
+    """Lean sweeps of the default fp64 K = 3 / 4 shapes and of the fp32 K = 3
+    pair shape store with the nt cache policy (profiles/nt_stores_r02.md);
+    K = 2, other fp32 shapes and explicit policies are left as given."""
     r = h3d.native().kernel_spec_resolved
     assert r("tl3", "fp64") == "tl3:1:3:1:16:0:3:2"
     assert r("tl4", "fp64") == "tl4:1:3:1:12:0:3:2"
@@ -289,4 +289,5 @@ def test_lean_store_policy_defaults(h3d):
     assert r("tl3:1:3:1:16:0:3:0", "fp64") == "tl3:1:3:1:16:0:3"
     assert r("tl3:1:3:1:16:0:3:19", "fp64") == "tl3:1:3:1:16:0:3:19"
     assert r("tl3:1:2:1:16", "fp64") == "tl3:1:2:1:16:0:3"
-    assert r("tl3", "fp32") == "tl3:2:3:1:16:0:3"
+    assert r("tl3", "fp32") == "tl3:2:3:1:16:0:3:2"
+    assert r("tl4", "fp32") == "tl4:2:2:1:16:0:3"
