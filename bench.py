@@ -76,6 +76,11 @@ def parse_args(argv=None):
                          "loopback); exercises the real RCCL send/recv/all-reduce path on a 1-GPU box")
     ap.add_argument("--timeout", type=float, default=1500.0,
                     help="watchdog (s): a launched job that runs longer is killed and exits non-zero")
+    ap.add_argument("--profile-sweeps", type=int, default=8,
+                    help="after the timed window, profile this many more sweeps per rank with timing "
+                         "events at the schedule's phase boundaries (JSON 'phases'; 0 disables)")
+    ap.add_argument("--watchdog", type=float, default=300.0,
+                    help="native watchdog (s): a rank whose peers stop making progress aborts its communicators")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -99,7 +104,7 @@ def launch(args, argv) -> int:
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   HEAT3D_BENCH_WORKER="1", HEAT3D_WATCHDOG_S=env.get("HEAT3D_WATCHDOG_S", "300"))
+                   HEAT3D_BENCH_WORKER="1")
         if args.rccl_host_split:
             env.update(NCCL_HOSTID=f"heat3d-bench-rank{r}", NCCL_SOCKET_IFNAME="lo")
         # each worker leads its own process group so that the watchdog can end
@@ -191,7 +196,8 @@ def run_rank(args) -> int:
                           decomp=dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
                           device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
-                          extra_args=["--temporal", str(args.temporal), "--kernel2", args.kernel2])
+                          extra_args=["--temporal", str(args.temporal), "--kernel2", args.kernel2,
+                                      "--watchdog", str(args.watchdog)])
 
     phase_log = os.environ.get("HEAT3D_BENCH_PHASES") == "1"
     tp = [time.perf_counter()]
@@ -248,6 +254,15 @@ def run_rank(args) -> int:
     reserved = s.native.reserved_cus
     placement = all_gather_objects({"rank": rank, "device": dev, "host": socket.gethostname(),
                                     "subdomain": list(s.native.local_subdomain(0)["n"])}, group)
+    # per-rank schedule profile, after (outside) the timed window: a few more
+    # sweeps of the same pipeline with timing events at its phase boundaries
+    # (interior / halo / boundary / all-reduce / check, compute-stream idle,
+    # how much of the halo + boundary chain ran under the interior)
+    prof = {}
+    if args.profile_sweeps > 0:
+        prof = {k: (round(v, 4) if isinstance(v, float) else v)
+                for k, v in s.native.profile_sweeps(args.profile_sweeps).items()}
+    phases = all_gather_objects(dict(rank=rank, **prof), group)
     del s
 
     ttc = None
@@ -303,6 +318,7 @@ def run_rank(args) -> int:
         "temporal_roofline_glups_per_gpu": round(5.6e12 / (2 * esize / max(1, K)) / 1e9, 1),
         "vs_temporal_roofline": round(value / world / (5.6e12 / (2 * esize / max(1, K)) / 1e9), 4),
         "time_to_converge": ttc,
+        "phases": phases,
         "baseline_note": "reference publishes no numbers (BASELINE.md); single-step roofline = "
                          "6.29 TB/s / (2*esize) per GPU",
     }

@@ -85,13 +85,25 @@ std::unique_ptr<Comm> make_socket_comm_from_table(int rank, int size, int listen
 std::unique_ptr<Comm> make_staged_comm(std::unique_ptr<Comm> inner);
 
 // Performance proxy: rank `rank` of a `size`-rank job alone on one device,
-// peers emulated (phantom_comm.cpp).
-std::unique_ptr<Comm> make_phantom_comm(int rank, int size);
+// peers emulated (phantom_comm.cpp): every exchange holds `channels`
+// workgroups per peer for bytes / gbps, every all-reduce
+// `allreduce_channels` workgroups for allreduce_us.
+struct PhantomOptions {
+  double gbps = 50.0, allreduce_us = 20.0;
+  int channels = 4, allreduce_channels = 2;
+};
+std::unique_ptr<Comm> make_phantom_comm(int rank, int size, const PhantomOptions& o = {});
 
 // RCCL: `unique_id` is the 128-byte ncclUniqueId from rank 0.
 bool rccl_available();
 std::string rccl_unique_id();
 std::string rccl_version();
-std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::string& unique_id, int device);
+// shared: one communicator for halos and all-reduces (else a second one from
+// ncclCommSplit); graph: its calls may be recorded into hipGraphs.
+struct RcclOptions {
+  bool shared = false, graph = false;
+};
+std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::string& unique_id, int device,
+                                     const RcclOptions& o = {});
 
 }  // namespace heat3d

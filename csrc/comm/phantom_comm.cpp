@@ -5,16 +5,15 @@
 // boundary kernels, deep halos, streams, lagged all-reduce), while the peers
 // are phantoms.  Received halos are filled with a same-sized face this rank
 // sends (numerically meaningless, finite), every exchange occupies the stream
-// for bytes-per-peer / HEAT3D_PHANTOM_GBPS, and every all-reduce for
-// HEAT3D_PHANTOM_ALLREDUCE_US.  Like RCCL, which moves p2p data with several
+// for bytes-per-peer / --phantom-gbps, and every all-reduce for
+// --phantom-allreduce-us.  Like RCCL, which moves p2p data with several
 // channels (one workgroup each) per peer, the emulated transfer holds
-// HEAT3D_PHANTOM_CHANNELS workgroups per peer (default 4) for its duration, and
+// --phantom-channels workgroups per peer (default 4) for its duration, and
 // the all-reduce one per ring channel (default 2): those workgroups must find
 // free CUs next to the interior sweep, exactly the contention a real run has.
 // Collectives are ordered like RCCL's (ordered_collectives).  This is how the
 // per-GPU time of the multi-GPU bench is measured on the one-GPU box
 // (tools/rank_proxy.py).
-#include <cstdlib>
 #include <map>
 
 #include "comm.hpp"
@@ -23,18 +22,11 @@ namespace heat3d {
 
 namespace {
 
-double env_or(const char* name, double dflt) {
-  const char* e = std::getenv(name);
-  return e && *e ? std::atof(e) : dflt;
-}
-
 class PhantomComm final : public Comm {
  public:
-  PhantomComm(int rank, int size)
-      : rank_(rank), size_(size), gbps_(env_or("HEAT3D_PHANTOM_GBPS", 50.0)),
-        ar_us_(env_or("HEAT3D_PHANTOM_ALLREDUCE_US", 20.0)),
-        channels_((int)env_or("HEAT3D_PHANTOM_CHANNELS", 4)),
-        ar_channels_((int)env_or("HEAT3D_PHANTOM_ALLREDUCE_CHANNELS", 2)) {
+  PhantomComm(int rank, int size, const PhantomOptions& o)
+      : rank_(rank), size_(size), gbps_(o.gbps), ar_us_(o.allreduce_us), channels_(o.channels),
+        ar_channels_(o.allreduce_channels) {
     HEAT3D_CHECK(rank >= 0 && rank < size, "phantom rank " << rank << " of " << size);
   }
   const char* name() const override { return "phantom"; }
@@ -75,8 +67,8 @@ class PhantomComm final : public Comm {
 
 }  // namespace
 
-std::unique_ptr<Comm> make_phantom_comm(int rank, int size) {
-  return std::unique_ptr<Comm>(new PhantomComm(rank, size));
+std::unique_ptr<Comm> make_phantom_comm(int rank, int size, const PhantomOptions& o) {
+  return std::unique_ptr<Comm>(new PhantomComm(rank, size, o));
 }
 
 }  // namespace heat3d

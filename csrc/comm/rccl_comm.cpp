@@ -83,7 +83,8 @@ void message_shape(std::size_t bytes, ncclDataType_t* dt, std::size_t* count) {
 
 class RcclComm final : public Comm {
  public:
-  RcclComm(int rank, int size, const std::string& uid, int device) : rank_(rank), size_(size) {
+  RcclComm(int rank, int size, const std::string& uid, int device, const RcclOptions& o)
+      : rank_(rank), size_(size), graph_(o.graph) {
     HEAT3D_CHECK(uid.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size " << uid.size());
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
@@ -92,11 +93,9 @@ class RcclComm final : public Comm {
     int n = 0;
     NCCL_CHECK(ncclCommCount(halo_, &n));
     HEAT3D_CHECK(n == size_, "RCCL communicator has " << n << " ranks, expected " << size_);
-    // A second communicator for the scalar all-reduce (HEAT3D_RCCL_SHARED=1
-    // forces the single-communicator form, which tests exercise).
-    const char* e = std::getenv("HEAT3D_RCCL_SHARED");
-    const bool force_shared = e && e[0] == '1';
-    if (force_shared || ncclCommSplit(halo_, 0, rank_, &red_, nullptr) != ncclSuccess || red_ == nullptr) {
+    // A second communicator for the scalar all-reduce (--rccl-shared forces
+    // the single-communicator form, which tests exercise).
+    if (o.shared || ncclCommSplit(halo_, 0, rank_, &red_, nullptr) != ncclSuccess || red_ == nullptr) {
       red_ = halo_;
       shared_ = true;
     }
@@ -110,12 +109,8 @@ class RcclComm final : public Comm {
   int size() const override { return size_; }
   std::vector<int> local_ranks() const override { return {rank_}; }
   bool device_buffers() const override { return true; }
-  // RCCL kernels inside a hipGraph capture have not been validated on this
-  // stack: graphs are refused unless HEAT3D_RCCL_GRAPH=1.
-  bool capturable() const override {
-    const char* e = std::getenv("HEAT3D_RCCL_GRAPH");
-    return e && e[0] == '1';
-  }
+  // RCCL calls are recorded into hipGraphs only with --rccl-graph
+  bool capturable() const override { return graph_; }
   int transport_ranks() const override {
     int n = 0;
     if (!halo_ || ncclCommCount(halo_, &n) != ncclSuccess) return -1;
@@ -182,14 +177,15 @@ class RcclComm final : public Comm {
  private:
   int rank_, size_;
   ncclComm_t halo_ = nullptr, red_ = nullptr;
-  bool shared_ = false;
+  bool shared_ = false, graph_ = false;
   void* bar_ = nullptr;
 };
 
 }  // namespace
 
-std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::string& unique_id, int device) {
-  return std::unique_ptr<Comm>(new RcclComm(rank, size, unique_id, device));
+std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::string& unique_id, int device,
+                                     const RcclOptions& o) {
+  return std::unique_ptr<Comm>(new RcclComm(rank, size, unique_id, device, o));
 }
 
 }  // namespace heat3d

@@ -89,10 +89,10 @@ std::string Config::usage() {
      << "  --graph / --no-graph      capture iterations in hipGraphs (default on)\n"
      << "  --no-overlap              do not split interior/boundary work\n"
      << "  --check-every K           host poll period of the device convergence flag\n"
-     << "  --kernel NAME             stencil kernel variant (auto|tile[:V:R:WZ:WY:L]|column|naive)\n"
+     << "  --kernel NAME             single-step kernel (auto|tile[:V:R:WZ:WY:L]|naive)\n"
      << "  --temporal 0|1|K          K-step temporal blocking, K = 2..6 (0 auto: on on the GPU for\n"
      << "                            one subdomain or x slabs; 1 off; results are bitwise identical)\n"
-     << "  --kernel2 SPEC  temporally blocked kernel: tb2, tbk2, tb3..tb6 (queue), tr2..tr6 (register ring) [:V:R:WZ:WY:L:Q]\n"
+     << "  --kernel2 SPEC            temporally blocked sweep kernel tl2..tl6[:V:R:WZ:WY:L:Q:STORE]\n"
      << "  --output PATH|none        Tecplot output (default output/out.dat for small grids)\n"
      << "  --tecplot-layout auto|ref|owned\n"
      << "  --compat                  reproduce reference reporting quirks\n"
@@ -109,6 +109,20 @@ std::string Config::usage() {
      << "  --reserve-cus N           CUs kept free of the interior sweep for comm / boundary / check\n"
      << "                            kernels (default: 8 = one per XCD when the overlapped\n"
      << "                            multi-rank schedule runs, else 0)\n"
+     << "  --lag auto|on|off         lagged convergence check of overlapped sweeps (3rd field buffer)\n"
+     << "  --no-block-overlap        block decompositions: exchange the halo first, then sweep\n"
+     << "  --no-long-sweeps          step-count remainders as partial sweeps, not K+1-step sweeps\n"
+     << "  --graph-multistream       record the overlapped multi-stream schedule into hipGraphs too\n"
+     << "  --no-rccl-graph           never record RCCL calls into hipGraphs (eager multi-rank steps)\n"
+     << "  --rccl-shared             one RCCL communicator for halos and all-reduces\n"
+     << "  --mem-reserve-gb G        memory preflight reserve (default 2)\n"
+     << "  --no-mem-preflight        skip the memory preflight\n"
+     << "  --host-mem-limit-gb G     host RAM budget of the gather-to-root Tecplot (default RAM/2)\n"
+     << "  --io-stage-mb M           output / checkpoint staging chunk (default 64)\n"
+     << "  --watchdog S              abort after S seconds without progress (default 900)\n"
+     << "  --fake-allreduce-us U     diagnostic: emulated all-reduce latency for virtual ranks\n"
+     << "  --phantom-gbps G --phantom-allreduce-us U --phantom-channels C --phantom-allreduce-channels C\n"
+     << "                            phantom-rank proxy (tools/rank_proxy.py) link emulation\n"
      << "  --quiet                   suppress the banner\n";
   return os.str();
 }
@@ -204,6 +218,31 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--threads") c.cpu_threads = (int)to_i64(get("--threads"), "--threads");
     else if (key == "--reserve-cus") c.reserve_cus = (int)to_i64(get("--reserve-cus"), "--reserve-cus");
     else if (key == "--quiet") c.quiet = true;
+    else if (key == "--lag") {
+      const std::string v = get("--lag");
+      if (v == "auto") c.lag = -1;
+      else if (v == "on" || v == "1") c.lag = 1;
+      else if (v == "off" || v == "0") c.lag = 0;
+      else throw UsageError("--lag must be auto, on or off");
+    }
+    else if (key == "--no-block-overlap") c.block_overlap = false;
+    else if (key == "--no-long-sweeps") c.long_sweeps = false;
+    else if (key == "--graph-multistream") c.graph_multistream = true;
+    else if (key == "--rccl-graph") c.rccl_graph = true;
+    else if (key == "--no-rccl-graph") c.rccl_graph = false;
+    else if (key == "--rccl-shared") c.rccl_shared = true;
+    else if (key == "--mem-reserve-gb") c.mem_reserve_gb = to_f64(get("--mem-reserve-gb"), "--mem-reserve-gb");
+    else if (key == "--no-mem-preflight") c.mem_preflight = false;
+    else if (key == "--host-mem-limit-gb") c.host_mem_limit_gb = to_f64(get("--host-mem-limit-gb"), "--host-mem-limit-gb");
+    else if (key == "--io-stage-mb") c.io_stage_mb = (int)to_i64(get("--io-stage-mb"), "--io-stage-mb");
+    else if (key == "--watchdog") c.watchdog_s = to_f64(get("--watchdog"), "--watchdog");
+    else if (key == "--fake-allreduce-us") c.fake_allreduce_us = to_f64(get("--fake-allreduce-us"), "--fake-allreduce-us");
+    else if (key == "--phantom-gbps") c.phantom_gbps = to_f64(get("--phantom-gbps"), "--phantom-gbps");
+    else if (key == "--phantom-allreduce-us")
+      c.phantom_allreduce_us = to_f64(get("--phantom-allreduce-us"), "--phantom-allreduce-us");
+    else if (key == "--phantom-channels") c.phantom_channels = (int)to_i64(get("--phantom-channels"), "--phantom-channels");
+    else if (key == "--phantom-allreduce-channels")
+      c.phantom_allreduce_channels = (int)to_i64(get("--phantom-allreduce-channels"), "--phantom-allreduce-channels");
     else if (key == "--help") throw UsageError("help requested");
     else throw UsageError("unknown option '" + a + "'");
   }
@@ -225,6 +264,8 @@ Config Config::parse(int argc, const char* const* argv) {
   if (c.check_every < 1) c.check_every = 1;
   if (c.graph_chunk < 2) c.graph_chunk = 2;
   if (c.graph_chunk % 2) c.graph_chunk += 1;
+  if (c.io_stage_mb < 1) c.io_stage_mb = 1;
+  if (c.watchdog_s <= 0) throw UsageError("--watchdog must be > 0");
   return c;
 }
 

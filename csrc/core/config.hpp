@@ -70,6 +70,24 @@ struct Config {
   int cpu_threads = 0;
   int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules
 
+  // --- schedule / runtime knobs (until round 2 HEAT3D_* environment variables)
+  int lag = -1;                   // lagged convergence check of overlapped sweeps (third buffer): -1 auto, 0 off, 1 on
+  bool block_overlap = true;      // block decompositions: interior || halo (false: exchange first)
+  bool long_sweeps = true;        // K+1-step sweeps absorb step counts that are not multiples of K
+  bool graph_multistream = false; // record the overlapped multi-stream schedule into hipGraphs too
+  bool rccl_graph = false;        // RCCL calls may be recorded into hipGraphs (single-stream schedules)
+  bool rccl_shared = false;       // one RCCL communicator for halos and all-reduces (else ncclCommSplit)
+  double mem_reserve_gb = 2.0;    // memory preflight: reserve for RCCL, code objects, scratch
+  bool mem_preflight = true;      // refuse configurations that do not fit before allocating
+  double host_mem_limit_gb = 0;   // gather-to-root Tecplot: host RAM budget (0 = half of RAM)
+  int io_stage_mb = 64;           // output / checkpoint staging chunk
+  double watchdog_s = 900;        // abort the communicators after this long without progress
+  double fake_allreduce_us = 0;   // diagnostic: emulated all-reduce latency (virtual ranks)
+  double phantom_gbps = 50;       // phantom-rank proxy: emulated link rate per peer
+  double phantom_allreduce_us = 20;
+  int phantom_channels = 4;       // workgroups an emulated transfer holds per peer
+  int phantom_allreduce_channels = 2;
+
   // Parse argv.  Throws UsageError on a malformed command line.
   static Config parse(int argc, const char* const* argv);
   static std::string usage();

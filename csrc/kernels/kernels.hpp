@@ -17,19 +17,22 @@
 namespace heat3d {
 
 struct KernelSpec {
-  // TB2 / TBK / TBR advance K time steps per HBM sweep: TB2 is the tuned K = 2
-  // kernel (stencil_tb2.hip), TBK the queue kernel (stencil_tbk.hip), TBR the
-  // register-ring kernel (stencil_tbr.hip; its 7th field is the T^n ring size)
-  // TBL: the lean K-step kernel (stencil_tbl.hip), halos as lanes / rows
-  enum Kind { Naive = 0, Column = 1, Tile = 2, TB2 = 3, TBK = 4, TBR = 5, TBL = 6 } kind = Tile;
+  // Tile: the single-step kernel (kernels_hip.hip; single steps, rollback
+  // recomputation, runs without temporal blocking).  Naive: one thread per
+  // point, the simplest gfx950 form (a test oracle).  TBL: the K-step
+  // temporally blocked lean kernel (stencil_tbl.hip; fp32 packed pairs in
+  // stencil_tbp.hip), K time steps per HBM sweep.  The round-1/2 queue and
+  // register-ring sweep kernels (tb2 / tbK / trK) were retired in round 3:
+  // no default path used them (docs/PERFORMANCE.md keeps their numbers).
+  enum Kind { Naive = 0, Tile = 2, TBL = 6 } kind = Tile;
   int K = 0;  // multi-step kinds: time steps per sweep
-  int WZ = 0, WY = 0;  // tile kernel: waves per workgroup along z and y
+  int WZ = 0, WY = 0;  // waves per workgroup along z and y
   int V = 0;  // elements per lane along z (0 = default for dtype)
   int R = 0;  // rows per wave along y (0 = default)
   int L = 0;  // x-segment length per wave (0 = auto)
-  int O = -1; // tile order: 1 = z tiles fastest (default), 0 = y tiles fastest
-  int NT = 0; // non-temporal output stores
-  bool multi_step() const { return kind == TB2 || kind == TBK || kind == TBR || kind == TBL; }
+  int O = -1; // TBL: output-store cache-policy bits (2 = nt)
+  int NT = 0; // TBL: T^n ring size
+  bool multi_step() const { return kind == TBL; }
   static KernelSpec parse(const std::string& s);
   std::string str() const;
   // zero (default) fields replaced by the tuned defaults for dtype t
@@ -52,10 +55,6 @@ struct StencilParams {
   int64_t ux[2] = {0, -1};
   // same for y and z (block decompositions with deep y / z halos)
   int64_t uy[2] = {0, -1}, uz[2] = {0, -1};
-  // multi-step kernels only: > 0 also updates the box shifted by xpair along
-  // x (the opposite boundary slab of an x slab), in the same launch where the
-  // kernel supports it (fp64 lean kernel), else as a second launch
-  int64_t xpair = 0;
 };
 
 struct InitParams {
@@ -80,21 +79,16 @@ H3D_HD inline double boundary_value(int64_t gi, int64_t gj, int64_t gk, const in
 namespace hip {
 void init_field(DType t, const InitParams& p, void* stream);
 void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
-// Two FTCS steps in one sweep (stencil_tb2.hip): p.in = T^n, p.out = T^{n+2};
-// residuals of the two steps go to slots p.slot and p.slot ^ 1.  The box must
-// be a whole subdomain whose ghosts are constant (Dirichlet) values.
-void stencil2(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
-// K-step temporally blocked sweep (stencil_tbk.hip), K = k.K
-void stencil_multi(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
-// Same sweep, register-ring kernel (stencil_tbr.hip)
-void stencil_ring(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
-// Same sweep, lean kernel (stencil_tbl.hip)
+// K-step temporally blocked sweep, lean kernel (stencil_tbl.hip), K = k.K
 void stencil_lean(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 // z tile stride of the lean kernel for a box (host-side choice, stencil_tbl.hip)
 int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U, int L);
 // fp32 lean kernel on packed pairs of z columns (stencil_tbp.hip; spec tlK:2:…)
 void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream);
-// Any multi-step kind (TB2 / TBK / TBR / TBL) -> its kernel
+bool lean_pair_supported(const KernelSpec& k);
+// Is the lean kernel variant that k resolves to for dtype t instantiated?
+bool lean_supported(DType t, const KernelSpec& k);
+// Any multi-step kind -> its kernel
 void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, void* stream);
 void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, void* stream);
@@ -129,9 +123,8 @@ void stencil(DType t, const StencilParams& p);
 // Definition of the K-step sweep kernels: K single steps through two scratch
 // fields (allocated by the caller, L.bytes() each).  Step s updates the box
 // widened by K-1-s planes into [ux0, ux1) and accumulates into residual slot
-// slot + s (tb2_slots: slot, slot ^ 1, the tuned 2-step kernel's convention).
-void stencil_multi(DType t, const StencilParams& p, int K, bool tb2_slots, void* scratch0,
-                   void* scratch1);
+// slot + s.
+void stencil_multi(DType t, const StencilParams& p, int K, void* scratch0, void* scratch1);
 void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf);
 void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf);
 void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,

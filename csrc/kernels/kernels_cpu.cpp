@@ -91,8 +91,7 @@ static void stencil_t(const StencilParams& p) {
   }
 }
 
-void stencil_multi(DType t, const StencilParams& p, int K, bool tb2_slots, void* scratch0,
-                   void* scratch1) {
+void stencil_multi(DType t, const StencilParams& p, int K, void* scratch0, void* scratch1) {
   if (p.state && p.state->done) return;
   void* scratch[2] = {scratch0, scratch1};
   std::memcpy(scratch[0], p.in, p.L.bytes());
@@ -102,7 +101,7 @@ void stencil_multi(DType t, const StencilParams& p, int K, bool tb2_slots, void*
     StencilParams a = p;
     a.in = s == 0 ? p.in : scratch[(s - 1) & 1];
     a.out = s == K - 1 ? p.out : scratch[s & 1];
-    a.slot = tb2_slots ? (s ? p.slot ^ 1 : p.slot) : p.slot + s;
+    a.slot = p.slot + s;
     // stage s computes the box widened by K-1-s into the deep halos (the
     // update range u of each axis), so that stage K-1 covers the box
     for (int ax = 0; ax < 3; ++ax)

@@ -5,23 +5,21 @@
 // terminating k loop — SURVEY.md §2.2) and the host loop nests around it
 // (T0 = T copy, face pack, residual scan, error scan: heat3D.cu:541-1106).
 //
-// Hot kernel: `stencil_column<Real,V,R>` — 2.5D blocking for a 7-point FTCS
-// update that is HBM-bound (16 B/point fp64, 8 B/point fp32):
-//   * one wave64 owns a (R rows in y) x (64*V points in z) column tile and
-//     marches along x over a segment of planes;
-//   * the x-1 / x / x+1 planes live in a register queue, prefetched one plane
-//     ahead, so every interior value is read from HBM exactly once;
-//   * z neighbours come from neighbouring lanes through DPP wave_shr/wave_shl
-//     (no LDS, no barriers), the two tile-edge values from one cooperative
-//     load + v_readlane;
-//   * y neighbours inside the tile are registers; the two tile-halo rows are
-//     re-read from L2 (shared with the y-adjacent wave, which the XCD-aware
-//     block remap keeps on the same XCD);
-//   * 16-byte vector loads/stores (rows are 128-B aligned, see layout.hpp);
-//   * the convergence residual max|T^{n+1}-T^n| is fused: wave max-reduce,
-//     one 64-bit atomic max per wave;
-//   * a device flag set by the convergence check turns the kernel into a
+// Single-step kernels (the K-step sweeps that run by default are in
+// stencil_tbl.hip / stencil_tbp.hip):
+//   * stencil_tile: a workgroup of WZ x WY waves marches a (rows x z) tile
+//     along x with the x-1 / x / x+1 planes in a register queue, z neighbours
+//     through DPP, y halo rows exchanged through LDS once per plane, 16-byte
+//     loads / stores, fused residual (NaN-propagating bit-pattern max, one
+//     commit per workgroup), XCD-aware block order.  Single steps, the
+//     rollback recomputation after convergence inside a sweep, and runs
+//     without temporal blocking;
+//   * stencil_naive: one lane per (y, z) column, seven loads per point — the
+//     simplest gfx950 form of the update, kept as an oracle;
+//   * a device flag set by the convergence check turns every kernel into a
 //     no-op, so over-issued / graph-replayed iterations are harmless.
+// Also here: IC/BC init, halo pack / unpack / copy, the convergence check,
+// the error reduction, checksums, the x-plan model of the sweep kernels.
 // Implicit contraction is disabled and the update's FMAs are explicit
 // (ftcs_update), so results are bitwise identical to the CPU backend
 // (kernels_cpu.cpp) and independent of the decomposition.
@@ -69,168 +67,10 @@ __global__ __launch_bounds__(256) void stencil_naive(const Real* __restrict__ in
   if (res) residual_commit(res, m);
 }
 
-// ---- column kernel ----------------------------------------------------------
-struct ColumnGeom {
-  int64_t z0a;       // first z of tile 0 (box z0 rounded down to V)
-  int nzt, nyt, nxs; // tiles along z, y; segments along x
-  int seg;           // planes per x segment
-  int64_t nwaves;    // nzt * nyt * nxs
-  int xq, xr;        // XCD remap: nblocks = 8 * xq + xr
-  int zfast;         // 1: consecutive waves take consecutive z tiles (whole rows per
-                     //    block pair -> DRAM-page / L2 locality); 0: consecutive y tiles
-  int nt;            // non-temporal (streaming) output stores
-};
-
-template <typename Real, int V, int R>
-__global__ __launch_bounds__(256) void stencil_column(const Real* __restrict__ in,
-                                                      Real* __restrict__ out, Layout L, Box b,
-                                                      ColumnGeom g, Real Dx, Real Dy, Real Dz,
-                                                      unsigned long long* res, const int* done) {
-  typedef typename VecOf<Real, V>::type Vec;
-  constexpr int TZ = 64 * V;
-  if (flag_set(done)) return;
-
-  // XCD-aware remap: blocks b and b+8 share an XCD under round-robin dispatch,
-  // so give each XCD a contiguous range of tiles (y-adjacent tiles share halo
-  // rows through that XCD's L2).  Performance only; any placement is correct.
-  const int blk = blockIdx.x;
-  const int xcd = blk & 7;
-  const int beff = xcd * g.xq + min(xcd, g.xr) + (blk >> 3);
-  int64_t t = (int64_t)beff * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (t >= g.nwaves) return;  // wave-uniform
-  const int lane = threadIdx.x & 63;
-  int yt, zt, xs;
-  if (g.zfast) {
-    zt = (int)(t % g.nzt);
-    t /= g.nzt;
-    yt = (int)(t % g.nyt);
-    xs = (int)(t / g.nyt);
-  } else {
-    yt = (int)(t % g.nyt);
-    t /= g.nyt;
-    zt = (int)(t % g.nzt);
-    xs = (int)(t / g.nzt);
-  }
-
-  const int64_t kb = g.z0a + (int64_t)zt * TZ;  // tile's first z
-  const int64_t k = kb + (int64_t)lane * V;     // this lane's first z
-  const int64_t yb = b.lo[1] + (int64_t)yt * R;
-  const int ract = (int)min((int64_t)R, b.hi[1] - yb);
-  const int64_t xa = b.lo[0] + (int64_t)xs * g.seg;
-  const int64_t xe = min(xa + (int64_t)g.seg, b.hi[0]);
-  const int64_t sx = L.sx, sy = L.sy;
-
-  // validity of this lane's V points
-  bool valid[V];
-  bool allvalid = true;
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    valid[v] = (k + v >= b.lo[2]) && (k + v < b.hi[2]);
-    allvalid &= valid[v];
-  }
-
-  // lane's column base pointer for row yb, plane 0
-  const int64_t base0 = L.index(0, yb, k);
-  // edge loads: lanes [0,R) fetch left edges (z = kb-1) of row `lane`,
-  // lanes [32,32+R) right edges (z = kb+TZ) of row `lane-32`
-  const int er = lane < 32 ? lane : lane - 32;
-  const bool eload = er < ract;
-  const int64_t ebase = L.index(0, yb + er, lane < 32 ? kb - 1 : kb + TZ);
-
-  auto ld = [&](int64_t plane, int r) -> Vec {
-    return *reinterpret_cast<const Vec*>(in + base0 + plane * sx + (int64_t)r * sy);
-  };
-
-  Vec qm[R], qc[R], qp[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-    if (r < ract) {
-      qm[r] = ld(xa - 1, r);
-      qc[r] = ld(xa, r);
-      qp[r] = ld(xa + 1, r);
-    }
-  Vec hb = ld(xa, -1), ht = ld(xa, ract);
-  Real ed = eload ? in[ebase + xa * sx] : Real(0);
-
-  double m = 0.0;
-  for (int64_t x = xa; x < xe; ++x) {
-    // prefetch plane x+2 centres and plane x+1 halos/edges
-    Vec qn[R];
-    const bool more = x + 1 < xe;
-    Vec hbn, htn;
-    Real edn = Real(0);
-    if (more) {
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (r < ract) qn[r] = ld(x + 2, r);
-      hbn = ld(x + 1, -1);
-      htn = ld(x + 1, ract);
-      if (eload) edn = in[ebase + (x + 1) * sx];
-    }
-
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r < ract) {
-        const Vec c = qc[r];
-        const Vec ym = r == 0 ? hb : qc[r > 0 ? r - 1 : 0];
-        const Vec yp = (r == ract - 1) ? ht : qc[r + 1 < R ? r + 1 : R - 1];
-        const Real left = readlane(ed, r);
-        const Real right = readlane(ed, 32 + r);
-        Vec zm, zp;
-        if constexpr (V == 1) {
-          zm = dpp_shr1(left, c);
-          zp = dpp_shl1(right, c);
-        } else {
-#pragma unroll
-          for (int v = 0; v < V; ++v) {
-            zm[v] = v == 0 ? dpp_shr1(left, c[V - 1]) : c[v - 1];
-            zp[v] = v == V - 1 ? dpp_shl1(right, c[0]) : c[v + 1];
-          }
-        }
-        Vec nv;
-        if constexpr (V == 1) {
-          nv = ftcs<Real>(c, qm[r], qp[r], ym, yp, zm, zp, Dx, Dy, Dz);
-          if (valid[0]) m = res_max(m, resid_abs(nv, c));
-        } else {
-#pragma unroll
-          for (int v = 0; v < V; ++v) {
-            nv[v] = ftcs<Real>(c[v], qm[r][v], qp[r][v], ym[v], yp[v], zm[v], zp[v], Dx, Dy, Dz);
-            if (valid[v]) m = res_max(m, resid_abs(nv[v], c[v]));
-          }
-        }
-        Real* dst = out + base0 + x * sx + (int64_t)r * sy;
-        if (allvalid) {
-          if (g.nt) __builtin_nontemporal_store(nv, reinterpret_cast<Vec*>(dst));
-          else *reinterpret_cast<Vec*>(dst) = nv;
-        } else {
-          if constexpr (V == 1) {
-            if (valid[0]) dst[0] = nv;
-          } else {
-#pragma unroll
-            for (int v = 0; v < V; ++v)
-              if (valid[v]) dst[v] = nv[v];
-          }
-        }
-      }
-    }
-    // rotate the register queue
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      qm[r] = qc[r];
-      qc[r] = qp[r];
-      qp[r] = qn[r];
-    }
-    hb = hbn;
-    ht = htn;
-    ed = edn;
-  }
-  if (res) residual_commit(res, m);
-}
-
 // ---- tile kernel: block-cooperative 2.5D blocking ---------------------------------
 // A workgroup of WZ x WY waves owns a (WY*R rows) x (WZ*64*V points) tile and
-// marches along x.  Each wave keeps its R x V column queue in registers as in
-// stencil_column, but the rows / edge points its neighbours need are
+// marches along x.  Each wave keeps its R x V column queue in registers, and
+// the rows / edge points its neighbours need are
 // exchanged through LDS once per plane (double-buffered by plane parity, one
 // s_barrier per plane).  Only the tile's outer halo (2 rows, 2 edge columns)
 // is fetched from memory, so HBM over-fetch drops from ~40 % (independent
@@ -598,64 +438,6 @@ static void launch_naive(const StencilParams& p, hipStream_t s) {
   HIPK_CHECK(hipGetLastError());
 }
 
-template <typename Real, int V, int R>
-static void launch_column(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
-  const Box& b = p.box;
-  constexpr int TZ = 64 * V;
-  int seg = k.L;
-  ColumnGeom g;
-  g.zfast = k.O < 0 ? 1 : k.O;
-  g.nt = k.NT;
-  g.z0a = (b.lo[2] / V) * V;
-  g.nzt = (int)((b.hi[2] - g.z0a + TZ - 1) / TZ);
-  g.nyt = (int)((b.extent(1) + R - 1) / R);
-  if (seg <= 0) {
-    // aim for >= ~16k waves so that 256 CUs see several rounds
-    const int64_t cols = (int64_t)g.nzt * g.nyt;
-    int64_t want = std::max<int64_t>(1, 16384 / std::max<int64_t>(1, cols));
-    seg = (int)std::max<int64_t>(16, (b.extent(0) + want - 1) / want);
-  }
-  g.seg = (int)std::min<int64_t>(seg, std::max<int64_t>(1, b.extent(0)));
-  g.nxs = (int)((b.extent(0) + g.seg - 1) / g.seg);
-  g.nwaves = (int64_t)g.nzt * g.nyt * g.nxs;
-  const int W = 4;
-  const int64_t nblocks = (g.nwaves + W - 1) / W;
-  HEAT3D_CHECK(nblocks < (1LL << 31), "too many blocks");
-  g.xq = (int)(nblocks / 8);
-  g.xr = (int)(nblocks % 8);
-  unsigned long long* res = p.state ? &p.state->residual[p.slot] : nullptr;
-  const int* done = p.state ? &p.state->done : nullptr;
-  hipLaunchKernelGGL((stencil_column<Real, V, R>), dim3((unsigned)nblocks), dim3(64 * W), 0, s,
-                     static_cast<const Real*>(p.in), static_cast<Real*>(p.out), p.L, b, g,
-                     (Real)p.D[0], (Real)p.D[1], (Real)p.D[2], res, done);
-  HIPK_CHECK(hipGetLastError());
-}
-
-template <typename Real>
-static void dispatch_column(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
-  const KernelSpec k = ks.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
-  const int V = k.V, R = k.R;
-  // Thin boxes (boundary shell slabs) go to the naive kernel: a column tile
-  // would run mostly idle lanes / rows there.
-  if (p.box.extent(2) < 32 || p.box.extent(1) < 2) {
-    launch_naive<Real>(p, s);
-    return;
-  }
-#define H3D_COL(VV, RR)                                  \
-  if (V == VV && R == RR) {                              \
-    launch_column<Real, VV, RR>(p, k, s);                \
-    return;                                              \
-  }
-  H3D_COL(1, 2) H3D_COL(1, 4) H3D_COL(1, 6) H3D_COL(1, 8) H3D_COL(2, 2) H3D_COL(2, 3)
-  H3D_COL(2, 4) H3D_COL(2, 6) H3D_COL(2, 8) H3D_COL(2, 12)
-  if constexpr (sizeof(Real) == 4) {
-    H3D_COL(4, 4) H3D_COL(4, 8)
-  }
-#undef H3D_COL
-  HEAT3D_THROW("unsupported column kernel variant V=" << V << " R=" << R << " for "
-               << (sizeof(Real) == 8 ? "fp64" : "fp32"));
-}
-
 template <typename Real>
 static void dispatch_tile(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   // defaults from the gfx950 sweep (KernelSpec::resolved, profiles/kernel_sweep.md)
@@ -686,12 +468,10 @@ void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream)
   if (k.kind == KernelSpec::Naive) {
     if (t == DType::F64) launch_naive<double>(p, S(stream));
     else launch_naive<float>(p, S(stream));
-  } else if (k.kind == KernelSpec::Tile) {
+  } else {
+    HEAT3D_CHECK(k.kind == KernelSpec::Tile, "single-step kernels: naive | tile");
     if (t == DType::F64) dispatch_tile<double>(p, k, S(stream));
     else dispatch_tile<float>(p, k, S(stream));
-  } else {
-    if (t == DType::F64) dispatch_column<double>(p, k, S(stream));
-    else dispatch_column<float>(p, k, S(stream));
   }
 }
 

@@ -53,8 +53,8 @@ struct TBLArgs {
   int ylo_live, yhi_live;      // y rows present in memory
   int c00, r00;                // first loaded column / row of tile (0, 0)
   int nzb, nyb;
-  int segsplit, n1, rb;        // x plan (TBRArgs encoding)
-  int zs;                      // tile stride along z = stored columns per tile (<= 64 - 2K) | tile order << 8
+  int segsplit, n1, rb;        // x plan: seg | split << 16, whole pieces, r | split-tail << 30
+  int zs;                      // tile stride along z = stored columns per tile (<= 64 - 2K)
 };
 
 namespace {
@@ -138,31 +138,16 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     pc = g.n1 + remap(blk - g.n1 - rr, rr);
     part = 2;
   }
-  // tile order inside an x segment: z fastest (py = 0), or z columns of py
-  // tile rows (bands), so that the workgroups an XCD runs at once form a
-  // compact patch whose shared halo rows / columns can hit its L2
-  const int zs = g.zs & 0xff, py = g.zs >> 8;
+  // tile order inside an x segment: z fastest
+  const int zs = g.zs;
   const int ntile = g.nzb * g.nyb;
   const int xs = pc / ntile;
   const int tt = pc - xs * ntile;
-  int zb, ybk;
-  if (py == 0) {
-    zb = tt % g.nzb;
-    ybk = tt / g.nzb;
-  } else {
-    const int band = tt / (g.nzb * py);
-    const int ylo = band * py;
-    const int pyb = min(py, g.nyb - ylo);
-    const int i = tt - band * g.nzb * py;
-    zb = i / pyb;
-    ybk = ylo + i % pyb;
-  }
+  const int zb = tt % g.nzb, ybk = tt / g.nzb;
   const int nxb = g.bhi[0] - g.blo[0];
   const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
-  // rb < 0: paired x slabs, segment xs starts at xs * split (StencilParams::xpair)
-  const bool xpaired = g.rb < 0;
-  int xlo_p = xs * (xpaired ? split : seg), xhi_p = min(xlo_p + seg, nxb);
-  if (!xpaired && part == 1 && (g.rb >> 30)) xhi_p = min(xhi_p, xlo_p + split);
+  int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
+  if (part == 1 && (g.rb >> 30)) xhi_p = min(xhi_p, xlo_p + split);
   if (part == 2) xlo_p = min(xlo_p + split, xhi_p);
 
   const int wave = sgpr(threadIdx.x >> 6);
@@ -360,15 +345,9 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
 // +4.6%; 512^3 would cross a round of workgroups and keeps 58), and only for
 // boxes of >= 500 x planes: the slab shares of the 4- and 8-GPU runs (250 and
 // 122 interior planes) lost 13% and 8% with it in the phantom-rank proxy
-// while the 2-GPU share (510 planes) gained 1.5% (tools/gpu_zs3.sh).
-// HEAT3D_TL_ZS forces a stride.
+// while the 2-GPU share (510 planes) gained 1.5%.
 int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U, int L) {
   const int wide = 64 - 2 * K;
-  static const int forced = [] {
-    const char* e = std::getenv("HEAT3D_TL_ZS");
-    return e && *e ? std::atoi(e) : 0;
-  }();
-  if (forced > 0 && forced <= wide) return forced;
   const int aligned = esize == 8 ? wide & ~7 : wide;
   if (aligned == wide || aligned <= 0 || nx < 500) return wide;
   const int64_t nyb = std::max<int64_t>(1, (ny + TY - 2 * K - 1) / (TY - 2 * K));
@@ -384,17 +363,7 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
 template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
 static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   constexpr bool swap_xy = SW;
-  // paired x slabs: the kernel's box is their hull, the x plan has exactly
-  // the two slabs as segments (each piece's window reproduces its own slab's
-  // update, count and store ranges; tests/test_gpu_temporal.py -k xpair)
   Box b = p.box;
-  const int64_t xpair = p.xpair;
-  HEAT3D_CHECK(!(xpair > 0 && swap_xy), "tl: paired slabs cannot march along y");
-  if (xpair > 0) {
-    HEAT3D_CHECK(xpair >= p.box.extent(0) && xpair < (1 << 15) && p.box.extent(0) < (1 << 15),
-                 "tl: paired x slabs overlap or are too far apart (" << xpair << ")");
-    b.hi[0] = p.box.lo[0] + xpair + p.box.extent(0);
-  }
   constexpr int TY = WY * R;
   // swap_xy: march along y with x as the tile rows (thin x slabs: a tile of
   // WY*R x-rows covers the slab and its K-deep halos, workgroups march the
@@ -446,29 +415,18 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
       device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW>), 64 * WY);
   constexpr int U = Q == 4 ? 12 : 6;  // the kernel's unroll (lcm(Q, 3, 2))
   const int ZS = lean_z_stride(b.extent(0), b.extent(1), b.extent(2), K, (int)sizeof(Real), TY, slots, U, ks.L);
-  static const int order_py = [] {  // HEAT3D_TL_PY: tile rows per band of the tile order (0 = z fastest)
-    const char* e = std::getenv("HEAT3D_TL_PY");
-    return e && *e ? std::max(0, std::min(255, std::atoi(e))) : 0;
-  }();
-  g.zs = ZS | (std::min(order_py, 255) << 8);
+  g.zs = ZS;
   g.c00 = (int)(b.lo[2] - K);
   g.r00 = (int)(b.lo[1] - K);
   g.nzb = (int)std::max<int64_t>(1, (b.extent(2) + ZS - 1) / ZS);
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
   const int64_t ntiles = (int64_t)g.nzb * g.nyb;
   const int64_t nxb = b.extent(0);
-  XPlan xp;
-  if (xpair > 0) {
-    xp.seg = (int)p.box.extent(0);
-    xp.split = (int)xpair;
-    xp.n1 = (int)(2 * ntiles);
-  } else {
-    xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
-  }
+  const XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
   HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
   g.segsplit = xp.seg | (xp.split << 16);
   g.n1 = xp.n1;
-  g.rb = xpair > 0 ? (int)0x80000000u : xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
+  g.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
   const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
   HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
   if (std::getenv("HEAT3D_TRACE"))
@@ -481,9 +439,8 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
                ? (int)a.localSizeBytes
                : 0;
   }();
-  static const bool allow = std::getenv("HEAT3D_ALLOW_SPILL") && std::getenv("HEAT3D_ALLOW_SPILL")[0] == '1';
-  HEAT3D_CHECK(spill == 0 || allow, "tl variant " << ks.str() << " spills " << spill
-                                                  << " B of registers per lane (HEAT3D_ALLOW_SPILL=1 overrides)");
+  // a spilling variant is refused (one was miscompiled on ROCm 7.2)
+  HEAT3D_CHECK(spill == 0, "tl variant " << ks.str() << " spills " << spill << " B of registers per lane");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
   hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
@@ -492,8 +449,9 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HIPK_CHECK(hipGetLastError());
 }
 
+// p == nullptr: only report whether the variant k resolves to exists
 template <typename Real>
-static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
+static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_t s) {
   const KernelSpec r = k.resolved(sizeof(Real) == 8 ? DType::F64 : DType::F32);
   const int K = k.K, R = r.R, WY = r.WY, Q = r.NT;
   // Thin x slabs (the K-plane boundary slabs of x-slab decompositions) with
@@ -501,58 +459,32 @@ static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_
   // (launch_tbl swap_xy) instead of 48-row tiles marching 3 planes plus a
   // 4-plane pipeline fill along x.  Phantom rank of the 1024^3 fp64 slab
   // bench (64 GB/s emulated links): 8 ranks 0.2135 -> 0.2084 ms per step, 4
-  // ranks 0.379 -> 0.359, 2 ranks unchanged (tools/gpu_swap.sh).
-  // HEAT3D_TL_SWAP=0 turns it off.
-  static const bool swap_ok = [] {
-    const char* e = std::getenv("HEAT3D_TL_SWAP");
-    return !(e && e[0] == '0');
-  }();
-  const Box& bx = p.box;
-  if (swap_ok && K == 3 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && p.xpair == 0 &&
-      bx.extent(0) > 0 && bx.extent(0) <= 2 * K && bx.extent(1) >= 16 * bx.extent(0)) {
-    if constexpr (sizeof(Real) == 8) launch_tbl<Real, 3, 3, 3, 3, 2, true>(p, k, s);
-    else launch_tbl<Real, 3, 3, 3, 3, 0, true>(p, k, s);
-    return;
-  }
-  // Medium x boxes (the interior of a thin slab share) with the default fp64
-  // tile: HEAT3D_TL_SWAP_X = N marches y when x <= N planes and y >= 4x.  A
-  // probe, off by default: one round of long y pieces instead of two rounds
-  // of x pieces lost on the phantom rank (8 ranks 0.2087 -> 0.2395 ms per
-  // step, 4 ranks 0.382 -> 0.475: 48-row bands over 122 / 250 x planes waste
-  // a third of a band, tools/gpu_swapx.sh).
-  static const int swap_x = [] {
-    const char* e = std::getenv("HEAT3D_TL_SWAP_X");
-    return e && *e ? std::atoi(e) : 0;
-  }();
-  if constexpr (sizeof(Real) == 8) {
-    if (swap_x > 0 && K == 3 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && p.xpair == 0 &&
-        bx.extent(0) <= swap_x && bx.extent(1) >= 4 * bx.extent(0)) {
-      launch_tbl<Real, 3, 16, 3, 3, 2, true>(p, k, s);
-      return;
+  // ranks 0.379 -> 0.359, 2 ranks unchanged (profiles/boundary_slabs_r02.md).
+  if (p) {
+    const Box& bx = p->box;
+    if (K == 3 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && bx.extent(0) > 0 && bx.extent(0) <= 2 * K &&
+        bx.extent(1) >= 16 * bx.extent(0)) {
+      if constexpr (sizeof(Real) == 8) launch_tbl<Real, 3, 3, 3, 3, 2, true>(*p, k, s);
+      else launch_tbl<Real, 3, 3, 3, 3, 0, true>(*p, k, s);
+      return true;
     }
   }
   if (sizeof(Real) == 4 && r.V == 2) {  // packed fp32 pairs (stencil_tbp.hip)
-    StencilParams a = p;
-    a.xpair = 0;
-    stencil_lean_pair(a, k, s);
-    if (p.xpair > 0) {  // its x plan has no paired form: second launch
-      a.box.lo[0] += p.xpair;
-      a.box.hi[0] += p.xpair;
-      stencil_lean_pair(a, k, s);
-    }
-    return;
+    if (!p) return lean_pair_supported(k);
+    stencil_lean_pair(*p, k, s);
+    return true;
   }
-  HEAT3D_CHECK(r.V == 1 && r.WZ == 1, "tl kernels: one value per lane (V = 1), one wave across z (WZ = 1)");
+  if (r.V != 1 || r.WZ != 1) return false;  // one value per lane, one wave across z
 #define H3D_TBL(RR, YY, KK, QQ)                                    \
   if (R == RR && WY == YY && K == KK && Q == QQ && r.O <= 0) {     \
-    launch_tbl<Real, RR, YY, KK, QQ>(p, k, s);                     \
-    return;                                                        \
+    if (p) launch_tbl<Real, RR, YY, KK, QQ>(*p, k, s);             \
+    return true;                                                   \
   }
   // output-store cache-policy bits (spec field 7: 2 = nt, 1 / 16 = sc0 / sc1), default shapes only
 #define H3D_TBLA(RR, YY, KK, AA)                                      \
   if (R == RR && WY == YY && K == KK && Q == 3 && r.O == (AA)) {      \
-    launch_tbl<Real, RR, YY, KK, 3, (AA)>(p, k, s);                   \
-    return;                                                           \
+    if (p) launch_tbl<Real, RR, YY, KK, 3, (AA)>(*p, k, s);           \
+    return true;                                                      \
   }
   H3D_TBLA(3, 16, 3, 2) H3D_TBLA(3, 16, 3, 3) H3D_TBLA(3, 16, 3, 17) H3D_TBLA(3, 16, 3, 18) H3D_TBLA(3, 16, 3, 19)
   H3D_TBLA(2, 16, 4, 2)  // the K = 4 default (long sweeps)
@@ -572,13 +504,26 @@ static void dispatch_tbl(const StencilParams& p, const KernelSpec& k, hipStream_
     H3D_TBL(4, 16, 6, 3) H3D_TBL(4, 16, 4, 4) H3D_TBL(3, 16, 5, 6)
   }
 #undef H3D_TBL
-  HEAT3D_THROW("unsupported tl kernel variant R=" << R << " WY=" << WY << " K=" << K << " Q=" << Q);
+  return false;
+}
+
+bool lean_supported(DType t, const KernelSpec& k) {
+  return t == DType::F64 ? dispatch_tbl<double>(nullptr, k, nullptr) : dispatch_tbl<float>(nullptr, k, nullptr);
 }
 
 void stencil_lean(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
   if (p.box.empty()) return;
-  if (t == DType::F64) dispatch_tbl<double>(p, k, S(stream));
-  else dispatch_tbl<float>(p, k, S(stream));
+  const bool ok = t == DType::F64 ? dispatch_tbl<double>(&p, k, S(stream)) : dispatch_tbl<float>(&p, k, S(stream));
+  if (!ok) {
+    const KernelSpec r = k.resolved(t);
+    HEAT3D_THROW("unsupported tl kernel variant V=" << r.V << " R=" << r.R << " WY=" << r.WY << " K=" << k.K
+                                                    << " Q=" << r.NT);
+  }
+}
+
+void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
+  HEAT3D_CHECK(k.kind == KernelSpec::TBL, "sweep needs a K-step kernel (tl2..tl6)");
+  stencil_lean(t, p, k, stream);
 }
 
 }  // namespace hip

@@ -347,11 +347,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
                "tl pair: y/z update range outside the ghosted layout");
   HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live + 1 && g.ulo <= b.lo[0] && g.uhi >= b.hi[0],
                "tl pair: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
-  static const int zs_env = [] {
-    const char* e = std::getenv("HEAT3D_TP_ZS");
-    return e && *e ? std::atoi(e) : 0;
-  }();
-  const int ZS = zs_env > 0 && zs_env <= 128 - 2 * K - 2 && zs_env % 2 == 0 ? zs_env : 128 - 2 * K - 2;
+  const int ZS = 128 - 2 * K - 2;
   g.zs = ZS;
   constexpr int YS = TY - 2 * K;
   g.r00 = (int)(b.lo[1] - K);
@@ -376,9 +372,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
                ? (int)a.localSizeBytes
                : 0;
   }();
-  static const bool allow = std::getenv("HEAT3D_ALLOW_SPILL") && std::getenv("HEAT3D_ALLOW_SPILL")[0] == '1';
-  HEAT3D_CHECK(spill == 0 || allow, "tl pair variant " << ks.str() << " spills " << spill
-                                                       << " B of registers per lane (HEAT3D_ALLOW_SPILL=1 overrides)");
+  HEAT3D_CHECK(spill == 0, "tl pair variant " << ks.str() << " spills " << spill << " B of registers per lane");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
   hipLaunchKernelGGL((stencil_tbp<R, WY, K, Q, AUX>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
@@ -387,29 +381,39 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HIPK_CHECK(hipGetLastError());
 }
 
-void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream) {
-  if (p.box.empty()) return;
+// p == nullptr: only report whether the variant k resolves to exists
+static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) {
   const KernelSpec r = k.resolved(DType::F32);
   const int K = k.K, R = r.R, WY = r.WY, Q = r.NT;
-  HEAT3D_CHECK(r.V == 2 && r.WZ == 1, "tl pair kernel: two values per lane (V = 2), one wave across z");
-  hipStream_t s = S(stream);
+  if (r.V != 2 || r.WZ != 1) return false;
 #define H3D_TBP(RR, YY, KK, QQ)                                \
   if (R == RR && WY == YY && K == KK && Q == QQ && r.O <= 0) {  \
-    launch_tbp<RR, YY, KK, QQ>(p, k, s);                       \
-    return;                                                    \
+    if (p) launch_tbp<RR, YY, KK, QQ>(*p, k, s);               \
+    return true;                                               \
   }
   // output-store cache policy (spec field 7), default shape only
 #define H3D_TBPA(AA)                                                       \
   if (R == 3 && WY == 16 && K == 3 && Q == 3 && r.O == (AA)) {             \
-    launch_tbp<3, 16, 3, 3, (AA)>(p, k, s);                                \
-    return;                                                                \
+    if (p) launch_tbp<3, 16, 3, 3, (AA)>(*p, k, s);                        \
+    return true;                                                           \
   }
   H3D_TBPA(2) H3D_TBPA(3) H3D_TBPA(17) H3D_TBPA(19)
 #undef H3D_TBPA
   H3D_TBP(3, 16, 3, 3) H3D_TBP(3, 16, 3, 4) H3D_TBP(2, 16, 3, 3) H3D_TBP(2, 16, 4, 3) H3D_TBP(2, 16, 4, 4)
   H3D_TBP(3, 16, 4, 3) H3D_TBP(2, 16, 2, 3) H3D_TBP(3, 16, 2, 3)
 #undef H3D_TBP
-  HEAT3D_THROW("unsupported tl pair variant R=" << R << " WY=" << WY << " K=" << K << " Q=" << Q);
+  return false;
+}
+
+bool lean_pair_supported(const KernelSpec& k) { return run_tbp(nullptr, k, nullptr); }
+
+void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream) {
+  if (p.box.empty()) return;
+  if (!run_tbp(&p, k, S(stream))) {
+    const KernelSpec r = k.resolved(DType::F32);
+    HEAT3D_THROW("unsupported tl pair variant V=" << r.V << " R=" << r.R << " WY=" << r.WY << " K=" << k.K
+                                                  << " Q=" << r.NT);
+  }
 }
 
 }  // namespace hip

@@ -106,10 +106,10 @@ std::unique_ptr<Solver> create_solver(const std::vector<std::string>& args, int 
     comm = make_local_comm(nranks);
   } else if (comm_kind == "rccl") {
     HEAT3D_CHECK(bk == BackendKind::Hip, "rccl comm needs the HIP backend");
-    comm = make_rccl_comm(rank, size, std::string(unique_id), dev);
+    comm = make_rccl_comm(rank, size, std::string(unique_id), dev, rccl_options(cfg));
     nranks = size;
   } else if (comm_kind == "phantom") {
-    comm = make_phantom_comm(rank, size);
+    comm = make_phantom_comm(rank, size, phantom_options(cfg));
     nranks = size;
   } else if (comm_kind == "socket" || comm_kind == "staged") {
     // a GPU backend always stages through host memory; "staged" forces the
@@ -389,11 +389,14 @@ PYBIND11_MODULE(_heat3d, m) {
     std::array<int64_t, 6> box = {0, n[0], 0, n[1], 0, n[2]};
     auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
     KernelSpec k = KernelSpec::parse(kernel);
-    if (!k.multi_step()) k.kind = KernelSpec::TB2;
+    if (!k.multi_step()) {  // two steps: the lean kernel at K = 2
+      k.kind = KernelSpec::TBL;
+      k.K = 2;
+    }
     hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
   });
   // multi-step sweep on a sub-box of a layout with gx ghost planes, u range ux
-  // (the solver's slab path); kernel = tb2 / tbk2 / tb3..tb6 spec
+  // (the solver's slab path); kernel = tl2..tl6 spec
   hk.def("stencil_sweep", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
                              int64_t gx, std::array<int64_t, 6> box, std::array<int64_t, 2> ux,
                              std::array<double, 3> D, int64_t state_ptr, int slot, const std::string& kernel,
@@ -404,23 +407,7 @@ PYBIND11_MODULE(_heat3d, m) {
     p.ux[0] = ux[0];
     p.ux[1] = ux[1];
     KernelSpec k = KernelSpec::parse(kernel);
-    if (!k.multi_step()) throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 / tr2..tr6 kernel");
-    hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
-  });
-  // the same on a pair of x slabs: box and box shifted by xpair along x
-  // (StencilParams::xpair: one launch for the fp64 lean kernel)
-  hk.def("stencil_sweep_xpair", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
-                                   int64_t gx, std::array<int64_t, 6> box, std::array<int64_t, 2> ux,
-                                   std::array<double, 3> D, int64_t state_ptr, int slot, const std::string& kernel,
-                                   int64_t xpair, int64_t stream) {
-    DType t = dt_of(dt);
-    auto p = sparams(in_ptr, out_ptr, n, (int64_t)dtype_size(t), box, D, state_ptr, slot);
-    p.L = to_layout(n, (int64_t)dtype_size(t), gx);
-    p.ux[0] = ux[0];
-    p.ux[1] = ux[1];
-    p.xpair = xpair;
-    KernelSpec k = KernelSpec::parse(kernel);
-    if (!k.multi_step()) throw UsageError("stencil_sweep_xpair needs a multi-step kernel");
+    if (!k.multi_step()) throw UsageError("stencil_sweep needs a tl2..tl6 kernel");
     hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
   });
   // deep ghosts on every axis (block decompositions): g = (gx, gy, gz),
@@ -438,7 +425,7 @@ PYBIND11_MODULE(_heat3d, m) {
       p.uz[e] = u[4 + e];
     }
     KernelSpec k = KernelSpec::parse(kernel);
-    if (!k.multi_step()) throw UsageError("stencil_sweep3 needs a tr2..tr6 kernel");
+    if (!k.multi_step()) throw UsageError("stencil_sweep3 needs a tl2..tl6 kernel");
     hip::sweep(t, p, k, reinterpret_cast<void*>(stream));
   });
   hk.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
@@ -491,10 +478,10 @@ PYBIND11_MODULE(_heat3d, m) {
     p.ux[0] = ux[0];
     p.ux[1] = ux[1];
     KernelSpec k = KernelSpec::parse(kernel);
-    if (!k.multi_step()) throw UsageError("stencil_sweep needs a tb2 / tbk2 / tb3..tb6 / tr2..tr6 kernel");
+    if (!k.multi_step()) throw UsageError("stencil_sweep needs a tl2..tl6 kernel");
     std::vector<char> s0(p.L.bytes()), s1(p.L.bytes());
     py::gil_scoped_release nogil;
-    cpu::stencil_multi(t, p, k.K, k.kind == KernelSpec::TB2, s0.data(), s1.data());
+    cpu::stencil_multi(t, p, k.K, s0.data(), s1.data());
   });
   ck.def("stencil_sweep3", [](const std::string& dt, int64_t in_ptr, int64_t out_ptr, std::array<int64_t, 3> n,
                               std::array<int64_t, 3> g, std::array<int64_t, 6> box, std::array<int64_t, 6> u,
@@ -508,10 +495,10 @@ PYBIND11_MODULE(_heat3d, m) {
       p.uz[e] = u[4 + e];
     }
     KernelSpec k = KernelSpec::parse(kernel);
-    if (!k.multi_step()) throw UsageError("stencil_sweep3 needs a tr2..tr6 kernel");
+    if (!k.multi_step()) throw UsageError("stencil_sweep3 needs a tl2..tl6 kernel");
     std::vector<char> s0(p.L.bytes()), s1(p.L.bytes());
     py::gil_scoped_release nogil;
-    cpu::stencil_multi(t, p, k.K, k.kind == KernelSpec::TB2, s0.data(), s1.data());
+    cpu::stencil_multi(t, p, k.K, s0.data(), s1.data());
   });
   ck.def("init_field", [](const std::string& dt, int64_t ptr, std::array<int64_t, 3> n, std::array<int64_t, 3> gstart,
                           std::array<int64_t, 3> N, std::array<double, 3> h) {
@@ -656,6 +643,16 @@ PYBIND11_MODULE(_heat3d, m) {
       })
       .def("set_phase_timing", &Solver::set_phase_timing)
       .def("phase_times", &Solver::phase_times)
+      .def("profile_sweeps", [](Solver& s, int n) {
+        std::vector<std::pair<std::string, double>> v;
+        {
+          py::gil_scoped_release nogil;
+          v = s.profile_sweeps(n);
+        }
+        py::dict d;
+        for (auto& kv : v) d[py::str(kv.first)] = kv.second;
+        return d;
+      }, py::arg("n") = 8)
       .def_property_readonly("num_local", &Solver::num_local)
       .def_property_readonly("is_root", &Solver::is_root)
       .def_property_readonly("process_rank", &Solver::process_rank)

@@ -78,8 +78,9 @@ class Backend {
   // kernels (see kernels.hpp)
   virtual void init_field(DType t, const InitParams& p, StreamId s) = 0;
   virtual void stencil(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) = 0;
-  // two steps T^n -> T^{n+2} (residual slots p.slot, p.slot^1)
-  virtual void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) = 0;
+  // K = k.K steps T^n -> T^{n+K} in one temporally blocked sweep (residual
+  // slots p.slot .. p.slot + K - 1)
+  virtual void sweep(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) = 0;
   virtual void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf,
                         StreamId s) = 0;
   virtual void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf,

@@ -71,27 +71,17 @@ class CpuBackend final : public Backend {
   }
   // Reference semantics of the K-step kernels: K single steps through two
   // scratch fields (same ghosts).  Step s updates the box widened by K-1-s
-  // planes into [ux0, ux1) and accumulates into residual slot `slot + s`
-  // (tb2: slots slot, slot ^ 1).
-  void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId sid) override {
-    if (p.xpair > 0) {  // paired x slabs: one after the other
-      StencilParams a = p;
-      a.xpair = 0;
-      stencil2(t, a, k, sid);
-      a.box.lo[0] += p.xpair;
-      a.box.hi[0] += p.xpair;
-      stencil2(t, a, k, sid);
-      return;
-    }
+  // planes into [ux0, ux1) and accumulates into residual slot `slot + s`.
+  void sweep(DType t, const StencilParams& p, const KernelSpec& k, StreamId) override {
     if (p.state && p.state->done) return;
-    const int K = k.kind == KernelSpec::TB2 ? 2 : k.K;
+    const int K = k.K;
     for (int i = 0; i < 2; ++i)
       if (scratch_bytes_[i] < p.L.bytes()) {
         release(scratch_[i]);
         scratch_[i] = alloc(p.L.bytes());
         scratch_bytes_[i] = p.L.bytes();
       }
-    cpu::stencil_multi(t, p, K, k.kind == KernelSpec::TB2, scratch_[0], scratch_[1]);
+    cpu::stencil_multi(t, p, K, scratch_[0], scratch_[1]);
   }
   ~CpuBackend() override {
     release(scratch_[0]);

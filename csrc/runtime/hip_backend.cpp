@@ -8,10 +8,13 @@
 // docs/ARCHITECTURE.md, minimal single-op patterns in
 // tools/graph_capture_repro.hip do not trigger it).  So the graph is built
 // explicitly: while recording, each operation is captured alone on a private
-// stream (a one-stream capture) into a child graph, added as a node that
-// depends on its stream's current frontier; an event record remembers the
-// recording stream's frontier and a wait merges it into the waiting stream's.
-// The resulting DAG has exactly the dependencies of the eager schedule.
+// per-stream capture stream straight into the graph being built
+// (hipStreamBeginCaptureToGraph) behind that stream's dependency frontier; an
+// event record remembers the recording stream's frontier and a wait merges it
+// into the waiting stream's.  The resulting DAG has exactly the dependencies
+// of the eager schedule.  (Round 2's alternatives — every operation a
+// child-graph node, or one-kernel captures re-added as kernel nodes — replayed
+// without overlap or broke ordering on HIP 7.2 and were removed.)
 //
 // The device is bound once (the reference called cudaSetDevice(rank % n) in
 // every iteration, heat3D.cu:650-654).  The comm and reduce streams get the
@@ -86,25 +89,16 @@ class HipBackend final : public Backend {
     if (!caps_[s]) HIP_CHECK(hipStreamCreateWithPriority(&caps_[s], hipStreamNonBlocking, prio_[s]));
     return caps_[s];
   }
-  hipStream_t child_capture_stream() {
-    if (!cap_) HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
-    return cap_;
-  }
   void drop_capture_streams() {
     for (auto& c : caps_)
       if (c) {
         (void)hipStreamDestroy(c);
         c = nullptr;
       }
-    if (cap_) {
-      (void)hipStreamDestroy(cap_);
-      cap_ = nullptr;
-    }
   }
   ~HipBackend() override {
     (void)hipSetDevice(dev_);
     if (rec_) (void)hipGraphDestroy(rec_);
-    if (cap_) (void)hipStreamDestroy(cap_);
     for (auto& s : caps_)
       if (s) (void)hipStreamDestroy(s);
     if (err_scratch_) (void)hipFree(err_scratch_);
@@ -144,32 +138,9 @@ class HipBackend final : public Backend {
       case CopyKind::D2D: kind = hipMemcpyDeviceToDevice; break;
       case CopyKind::H2H: kind = hipMemcpyHostToHost; break;
     }
-    if (recording_ && flatten_) {  // a memcpy node of the graph itself
-      HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
-      auto& t = tail_[s];
-      hipGraphNode_t node = nullptr;
-      HIP_CHECK(hipGraphAddMemcpyNode1D(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), dst, src, bytes, kind));
-      t.assign(1, node);
-      return;
-    }
     op(s, [&](hipStream_t st) { HIP_CHECK(hipMemcpyAsync(dst, src, bytes, kind, st)); });
   }
   void memset(void* dst, int v, std::size_t bytes, StreamId s) override {
-    if (recording_ && flatten_) {  // a memset node of the graph itself
-      HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
-      hipMemsetParams p{};
-      p.dst = dst;
-      p.elementSize = 1;
-      p.height = 1;
-      p.pitch = 0;
-      p.value = (unsigned)(v & 0xff);
-      p.width = bytes;
-      auto& t = tail_[s];
-      hipGraphNode_t node = nullptr;
-      HIP_CHECK(hipGraphAddMemsetNode(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), &p));
-      t.assign(1, node);
-      return;
-    }
     op(s, [&](hipStream_t st) { HIP_CHECK(hipMemsetAsync(dst, v, bytes, st)); });
   }
 
@@ -195,60 +166,27 @@ class HipBackend final : public Backend {
     HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
     in_op_ = true;
     op_s_ = s;
-    if (rmode_ == kToGraph) {
-      // capture straight into the recorded graph, behind the stream's frontier
-      auto& t = tail_[s];
-      HIP_CHECK(hipStreamBeginCaptureToGraph(capture_stream(s), rec_, t.empty() ? nullptr : t.data(), nullptr, t.size(),
-                                             hipStreamCaptureModeThreadLocal));
-      return caps_[s];
-    }
-    HIP_CHECK(hipStreamBeginCapture(child_capture_stream(), hipStreamCaptureModeThreadLocal));
-    return cap_;
+    // capture straight into the recorded graph, behind the stream's frontier
+    auto& t = tail_[s];
+    HIP_CHECK(hipStreamBeginCaptureToGraph(capture_stream(s), rec_, t.empty() ? nullptr : t.data(), nullptr, t.size(),
+                                           hipStreamCaptureModeThreadLocal));
+    return caps_[s];
   }
   void op_end(StreamId s) override {
     if (!recording_) return;
     HEAT3D_CHECK(in_op_ && op_s_ == s, "graph recording: unbalanced operation");
     in_op_ = false;
     hipGraph_t g = nullptr;
-    if (rmode_ == kToGraph) {
-      // the new frontier: the capture's dependency set after the operation
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      const hipGraphNode_t* deps = nullptr;
-      std::size_t nd = 0;
-      hipError_t e = hipStreamGetCaptureInfo_v2(caps_[s], &cs, nullptr, nullptr, &deps, &nd);
-      std::vector<hipGraphNode_t> front(deps, deps + (e == hipSuccess ? nd : 0));
-      hipError_t e2 = hipStreamEndCapture(caps_[s], &g);
-      HIP_CHECK(e);
-      HIP_CHECK(e2);
-      if (!front.empty()) tail_[s] = std::move(front);
-      return;
-    }
-    HIP_CHECK(hipStreamEndCapture(cap_, &g));
-    std::size_t n = 0;
-    hipError_t e = hipGraphGetNodes(g, nullptr, &n);
-    if (e == hipSuccess && n > 0) {
-      hipGraphNode_t node = nullptr;
-      auto& t = tail_[s];
-      // a one-kernel operation becomes a kernel node of the graph itself (the
-      // runtime keeps a flat graph's independent branches on parallel
-      // streams); anything else (copies, multi-node captures) a child graph
-      bool flat = false;
-      if (n == 1 && flatten_) {
-        hipGraphNode_t only = nullptr;
-        hipGraphNodeType ty;
-        hipKernelNodeParams kp;
-        if (hipGraphGetNodes(g, &only, &n) == hipSuccess && hipGraphNodeGetType(only, &ty) == hipSuccess &&
-            ty == hipGraphNodeTypeKernel && hipGraphKernelNodeGetParams(only, &kp) == hipSuccess) {
-          e = hipGraphAddKernelNode(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), &kp);
-          flat = true;
-
-        }
-      }
-      if (!flat) e = hipGraphAddChildGraphNode(&node, rec_, t.empty() ? nullptr : t.data(), t.size(), g);
-      if (e == hipSuccess) t.assign(1, node);
-    }
-    (void)hipGraphDestroy(g);
+    // the new frontier: the capture's dependency set after the operation
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipGraphNode_t* deps = nullptr;
+    std::size_t nd = 0;
+    hipError_t e = hipStreamGetCaptureInfo_v2(caps_[s], &cs, nullptr, nullptr, &deps, &nd);
+    std::vector<hipGraphNode_t> front(deps, deps + (e == hipSuccess ? nd : 0));
+    hipError_t e2 = hipStreamEndCapture(caps_[s], &g);
     HIP_CHECK(e);
+    HIP_CHECK(e2);
+    if (!front.empty()) tail_[s] = std::move(front);
   }
   Event event_create() override {
     hipEvent_t e;
@@ -312,7 +250,7 @@ class HipBackend final : public Backend {
     evn_.clear();
     drop_capture_streams();
     hipGraphExec_t ex = nullptr;
-    hipError_t e = hipGraphInstantiateWithFlags(&ex, g, rmode_ == kToGraph ? hipGraphInstantiateFlagUseNodePriority : 0);
+    hipError_t e = hipGraphInstantiateWithFlags(&ex, g, hipGraphInstantiateFlagUseNodePriority);
     (void)hipGraphDestroy(g);
     HIP_CHECK(e);
     // upload now (ordered on the compute stream) so that the first launch
@@ -333,7 +271,7 @@ class HipBackend final : public Backend {
   void stencil(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) override {
     op(s, [&](hipStream_t st) { hip::stencil(t, p, k, st); });
   }
-  void stencil2(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) override {
+  void sweep(DType t, const StencilParams& p, const KernelSpec& k, StreamId s) override {
     op(s, [&](hipStream_t st) { hip::sweep(t, p, k, st); });
   }
   void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, StreamId s) override {
@@ -391,12 +329,7 @@ class HipBackend final : public Backend {
   void abort_op() {
     in_op_ = false;
     hipGraph_t g = nullptr;
-    if (rmode_ == kToGraph) {
-      (void)hipStreamEndCapture(caps_[op_s_], &g);  // g is rec_, owned by the recorder
-    } else {
-      (void)hipStreamEndCapture(cap_, &g);
-      if (g) (void)hipGraphDestroy(g);
-    }
+    (void)hipStreamEndCapture(caps_[op_s_], &g);  // g is rec_, owned by the recorder
     (void)hipGetLastError();
   }
 
@@ -408,22 +341,8 @@ class HipBackend final : public Backend {
   bool recording_ = false, in_op_ = false;
   StreamId op_s_ = kCompute;
   hipGraph_t rec_ = nullptr;
-  hipStream_t cap_ = nullptr;                        // private one-operation capture stream
   std::vector<hipGraphNode_t> tail_[kNumStreams];    // dependency frontier per stream
   hipStream_t caps_[kNumStreams] = {nullptr, nullptr, nullptr};
-  // how operations enter the recorded graph (HEAT3D_GRAPH_RECORD):
-  //   graph (default): captured straight into it (hipStreamBeginCaptureToGraph)
-  //   flat: captured alone, one-kernel captures re-added as kernel nodes,
-  //         copies / memsets added as nodes
-  //   child: every operation a child-graph node (HIP 7.2 replays those on the
-  //          launch stream only: no overlap, profiles/rank_proxy_r02.md)
-  enum RecordMode { kToGraph, kFlat, kChild };
-  const RecordMode rmode_ = [] {
-    const char* e = std::getenv("HEAT3D_GRAPH_RECORD");
-    const std::string v = e ? e : "";
-    return v == "child" ? kChild : v == "flat" ? kFlat : kToGraph;
-  }();
-  const bool flatten_ = rmode_ == kFlat;
   std::unordered_map<Event, std::vector<hipGraphNode_t>> evn_;  // event -> frontier at record
   double* err_scratch_ = nullptr;
   Roctx roctx_;

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
+#include <map>
 #include <sstream>
 #include <thread>
 
@@ -60,31 +61,13 @@ KernelSpec KernelSpec::parse(const std::string& s) {
   std::stringstream ss(s);
   std::string p;
   while (std::getline(ss, p, ':')) parts.push_back(p);
-  if (parts[0] == "naive") {
+  const std::string& h = parts[0];
+  if (h == "naive") {
     k.kind = Naive;
-  } else if (parts[0] == "column") {
-    k.kind = Column;
-    if (parts.size() > 1) k.V = std::atoi(parts[1].c_str());
-    if (parts.size() > 2) k.R = std::atoi(parts[2].c_str());
-    if (parts.size() > 3) k.L = std::atoi(parts[3].c_str());
-    if (parts.size() > 4) k.O = std::atoi(parts[4].c_str());
-    if (parts.size() > 5) k.NT = std::atoi(parts[5].c_str());
-  } else if (parts[0] == "tile" || parts[0] == "tb2" || parts[0] == "tbk2" ||
-             (parts[0].size() == 3 && parts[0][0] == 't' && parts[0][1] == 'b' && parts[0][2] >= '3' &&
-              parts[0][2] <= '6') ||
-             (parts[0].size() == 3 && parts[0][0] == 't' && (parts[0][1] == 'r' || parts[0][1] == 'l') &&
-              parts[0][2] >= '2' && parts[0][2] <= '6')) {
-    // tile = single step; tb2 = tuned 2-step kernel; tb3..tb6 / tbk2 = K-step
-    // queue kernel; tr2..tr6 = K-step register-ring kernel; tl2..tl6 = lean
-    // K-step kernel
-    k.kind = parts[0] == "tile" ? Tile
-             : parts[0] == "tb2" ? TB2
-             : parts[0][1] == 'r' ? TBR
-             : parts[0][1] == 'l' ? TBL
-                                  : TBK;
-    if (k.kind == TB2) k.K = 2;
-    if (k.kind == TBK) k.K = parts[0] == "tbk2" ? 2 : parts[0][2] - '0';
-    if (k.kind == TBR || k.kind == TBL) k.K = parts[0][2] - '0';
+  } else if (h == "tile" || (h.size() == 3 && h[0] == 't' && h[1] == 'l' && h[2] >= '2' && h[2] <= '6')) {
+    // tile = single step; tl2..tl6 = K-step lean sweep kernel
+    k.kind = h == "tile" ? Tile : TBL;
+    if (k.kind == TBL) k.K = h[2] - '0';
     auto at = [&](std::size_t i) { return parts.size() > i ? std::atoi(parts[i].c_str()) : 0; };
     k.V = at(1);
     k.R = at(2);
@@ -92,11 +75,13 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     k.WY = at(4);
     k.L = at(5);
     k.NT = at(6);
-    if ((k.kind == TBR || k.kind == TBL) && parts.size() > 7) k.O = at(7);  // tr: 1 = non-temporal output stores; tl: store cache-policy bits
+    if (k.kind == TBL && parts.size() > 7) k.O = at(7);  // store cache-policy bits
+  } else if (h == "column" || h == "tb2" || h == "tbk2" || (h.size() == 3 && h[0] == 't' && (h[1] == 'b' || h[1] == 'r'))) {
+    throw UsageError("kernel '" + s + "' was retired in round 3 (the column / queue / register-ring kernels); "
+                     "use tile for single steps and tl2..tl6 for K-step sweeps");
   } else {
-    throw UsageError("unknown kernel '" + s +
-                     "' (auto | naive | column[:V[:R[:L[:O[:NT]]]]] | tile|tb2..tb6|tbk2|tr2..tr6|tl2..tl6"
-                     "[:V[:R[:WZ[:WY[:L[:NT]]]]]])");
+    throw UsageError("unknown kernel '" + s + "' (auto | naive | tile[:V[:R[:WZ[:WY]]]] | "
+                     "tl2..tl6[:V[:R[:WZ[:WY[:L[:Q[:STORE]]]]]]])");
   }
   return k;
 }
@@ -108,39 +93,11 @@ KernelSpec KernelSpec::resolved(DType t) const {
     if (f == 0) f = v;
   };
   switch (kind) {
-    case Column:
-      def(r.V, f64 ? 2 : 4);
-      def(r.R, 8);
-      break;
     case Tile:  // 8-wave tiles, 16 rows x 512 points
       def(r.V, f64 ? 2 : 4);
       def(r.R, 8);
       def(r.WZ, f64 ? 4 : 2);
       def(r.WY, 2);
-      break;
-    case TB2:  // one wave per tile column, 8 waves of 2 rows
-      def(r.V, f64 ? 2 : 4);
-      def(r.R, 2);
-      def(r.WZ, 1);
-      def(r.WY, 8);
-      break;
-    case TBK:  // 64-row tiles of 16 waves (fp64, V=1) / 32-row tiles of 8 waves (fp32)
-      def(r.V, f64 ? 1 : 2);
-      def(r.R, 4);
-      def(r.WZ, 1);
-      def(r.WY, f64 ? 16 : 8);
-      def(r.NT, 1);  // prefetch depth
-      break;
-    case TBR:  // 7th field = T^n ring size.  fp64: K = 2 64 x 64 tiles, K = 3
-               // 48 x 64, K >= 4 32 x 64 (8 waves); fp32: 32 x 128.  All
-               // without register spills (launch_tbr refuses spilling variants;
-               // the former K = 2 fp64 default 2:2:1:16 spills since the y / z
-               // update ranges).
-      def(r.V, f64 ? 1 : 2);
-      def(r.R, f64 ? (K == 3 ? 3 : 4) : 4);
-      def(r.WZ, 1);
-      def(r.WY, f64 ? (K <= 3 ? 16 : 8) : 8);
-      def(r.NT, 3);
       break;
     case TBL:  // lean kernel: 16 waves of 64 columns.  fp64: 3 rows per wave
                // (48-row tiles), 2 from K = 4 (32-row tiles: 115 VGPRs, no
@@ -150,7 +107,7 @@ KernelSpec KernelSpec::resolved(DType t) const {
       def(r.V, f64 || K > 4 ? 1 : 2);
       // fp64 K = 4 (the long sweeps of step counts that are not multiples of
       // 3): 12 waves of 3 rows, 144 VGPRs, 750 vs 719 GLUPS for 16 x 2 rows
-      // with nt stores on one box (tools/gpu_k4.sh)
+      // with nt stores on one box
       if (f64 && K == 4 && r.V == 1 && r.R == 0 && r.WY == 0) {
         r.R = 3;
         r.WY = 12;
@@ -162,12 +119,12 @@ KernelSpec KernelSpec::resolved(DType t) const {
       // fp64 default shape: non-temporal output stores (the sweep's output is
       // not re-read before the next sweep; streaming it past L2 keeps the
       // input halo lines resident).  MI355X, 1024^3 kernel level: 756 -> 798
-      // GLUPS, 512^3 / 768^3 +2-2.5%; fp32 pair kernel unchanged (tools/gpu_nt.sh)
+      // GLUPS, 512^3 / 768^3 +2-2.5%
       // (also K = 4, the long sweeps of step counts that are not multiples of
       // 3: 5.45 -> 5.38 ms per 1024^3 sweep.  Not K = 2: its partial sweep went
       // from 3.96 to 5.45 ms with nt stores; profiles/bench_r02_driver_gap.md)
       // fp32 packed-pair default shape too: 1388 -> 1431 GLUPS at 1024^3, 1354
-      // -> 1513 at 2049^3 (tools/gpu_tpzs.sh)
+      // -> 1513 at 2049^3
       if (!f64 && r.O < 0 && r.V == 2 && K == 3 && r.R == 3 && r.WY == 16 && r.NT == 3) r.O = 2;
       if (f64 && r.O < 0 && r.V == 1 && r.NT == 3 &&
           ((K == 3 && r.R == 3 && r.WY == 16) || (K == 4 && r.R == 2 && r.WY == 16) ||
@@ -182,20 +139,10 @@ KernelSpec KernelSpec::resolved(DType t) const {
 
 std::string KernelSpec::str() const {
   if (kind == Naive) return "naive";
-  if (kind == Tile || multi_step()) {
-    std::ostringstream os;
-    os << (kind == Tile  ? std::string("tile:")
-           : kind == TB2 ? std::string("tb2:")
-           : kind == TBR ? "tr" + std::to_string(K) + ":"
-           : kind == TBL ? "tl" + std::to_string(K) + ":"
-           : K == 2      ? std::string("tbk2:")
-                         : "tb" + std::to_string(K) + ":")
-       << V << ":" << R << ":" << WZ << ":" << WY << ":" << L << ":" << NT;
-    if ((kind == TBR && O == 1) || (kind == TBL && O > 0)) os << ":" << O;
-    return os.str();
-  }
   std::ostringstream os;
-  os << "column:" << V << ":" << R << ":" << L << ":" << O << ":" << NT;
+  os << (kind == Tile ? std::string("tile:") : "tl" + std::to_string(K) + ":") << V << ":" << R << ":" << WZ << ":"
+     << WY << ":" << L << ":" << NT;
+  if (kind == TBL && O > 0) os << ":" << O;
   return os.str();
 }
 
@@ -215,32 +162,25 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
                                << comm_->size() << " ranks");
   dec_ = Decomposition::make(cfg_.n, dims);
   kspec_ = KernelSpec::parse(cfg_.kernel);
-  if (kspec_.kind == KernelSpec::TB2) kspec_.kind = KernelSpec::Tile;
+  if (kspec_.kind == KernelSpec::TBL) kspec_.kind = KernelSpec::Tile;
   kspec2_ = KernelSpec::parse(cfg_.kernel2);
   overlap_ = cfg_.overlap;
 
   // K-step temporal blocking: on by default on the GPU, opt-in on the CPU
-  // backend (tests).  Depth K from --temporal K, else from --kernel2 tbK,
+  // backend (tests).  Depth K from --temporal K, else from --kernel2 tlK,
   // else kDefaultTemporal.  Halos travel K planes / rows / columns deep, so
   // every subdomain needs >= K owned points along each split axis.  y / z
-  // splits (block decompositions) need the register-ring kernel (the only one
-  // with y / z update ranges) and an axis-ordered exchange that also fills
-  // the edge and corner ghosts a K-step update reads.  Decided from the
-  // global decomposition so that every rank agrees.
-  // Auto depth: 3, for one subdomain and for x slabs alike (MI355X, 1024^3
-  // fp64 as 8 virtual x slabs on one GPU: K = 3 341 GLUPS vs K = 2 301 with the
-  // ring kernel; profiles/kernel_sweep.md)
+  // splits (block decompositions) use the kernel's y / z update ranges and an
+  // axis-ordered exchange that also fills the edge and corner ghosts a K-step
+  // update reads.  Decided from the global decomposition so that every rank
+  // agrees.  Auto depth: 3, for one subdomain and for x slabs alike.
   int K = cfg_.temporal >= 2 ? cfg_.temporal
           : kspec2_.multi_step() ? kspec2_.K
           : dt_ == DType::F64    ? kDefaultTemporal
                                  : kDefaultTemporalF32;
-  // default kernel: the lean kernel (stencil_tbl.hip; MI355X 1024^3, same box:
-  // fp64 tl3 740-746 vs ring tr3 726-732 GLUPS; fp32 its packed-pair form
-  // stencil_tbp.hip, tl3:2:3 1450 vs tl4:1:4 1288),
-  // except at K = 2 where the tuned queue kernel tb2 is used; tb2 / tbK /
-  // trK / tlK force one
-  if (!kspec2_.multi_step()) kspec2_.kind = K == 2 ? KernelSpec::TB2 : KernelSpec::TBL;
-  if (kspec2_.kind == KernelSpec::TB2 && K != 2) kspec2_.kind = KernelSpec::TBK;
+  // the sweep kernel: the lean kernel (stencil_tbl.hip; fp32 its packed-pair
+  // form, stencil_tbp.hip); --kernel2 tlK:... picks a variant
+  kspec2_.kind = KernelSpec::TBL;
   kspec2_.K = K;
   int64_t min_n[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
   for (const auto& sd : dec_.subs)
@@ -249,12 +189,6 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   bool fits = true;
   for (int a = 0; a < 3; ++a) fits &= dims[a] == 1 || min_n[a] >= K;
   tb_ = kspec_.kind != KernelSpec::Naive && (cfg_.temporal >= 2 || (cfg_.temporal == 0 && be_->is_gpu())) && fits;
-  if (tb_ && block) {
-    if (cfg_.kernel2.empty() || cfg_.kernel2 == "auto") kspec2_.kind = KernelSpec::TBL;
-    if (kspec2_.kind != KernelSpec::TBR && kspec2_.kind != KernelSpec::TBL)
-      throw UsageError("temporal blocking with y/z neighbours needs a kernel with y/z update ranges "
-                       "(--kernel2 trK or tlK)");
-  }
   K_ = tb_ ? K : 1;
   for (int a = 0; a < 3; ++a) hd_[a] = tb_ && dims[a] > 1 ? K : 1;
   halo_depth_ = hd_[0];
@@ -263,24 +197,21 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   // of every split axis; otherwise exchange first, then sweep
   bool thick = true;
   for (int a = 0; a < 3; ++a) thick &= dims[a] == 1 || min_n[a] >= 2 * K + 1;
-  const char* ebo = std::getenv("HEAT3D_BLOCK_OVERLAP");
-  const bool block_overlap = !(ebo && ebo[0] == '0');
-  tb_overlap_ = tb_ && dims[0] * dims[1] * dims[2] > 1 && overlap_ && thick && (!block || block_overlap);
+  tb_overlap_ = tb_ && dims[0] * dims[1] * dims[2] > 1 && overlap_ && thick && (!block || cfg_.block_overlap);
   // lagged convergence check (third buffer, two residual-slot banks) keeps
   // the all-reduce + check off the critical path of the overlapped sweeps
-  {
-    const char* e = std::getenv("HEAT3D_LAG");
-    lag_ = tb_overlap_ && 2 * K_ <= kResidualSlots && !(e && e[0] == '0');
-  }
+  if (cfg_.lag == 1 && !(tb_overlap_ && 2 * K_ <= kResidualSlots))
+    throw UsageError("--lag on needs overlapped temporally blocked sweeps of depth K <= " +
+                     std::to_string(kResidualSlots / 2));
+  lag_ = tb_overlap_ && 2 * K_ <= kResidualSlots && cfg_.lag != 0;
   nbuf_ = lag_ ? 3 : 2;
-  if (const char* e = std::getenv("HEAT3D_FAKE_ALLREDUCE_US")) fake_allreduce_us_ = std::atof(e);
+  fake_allreduce_us_ = cfg_.fake_allreduce_us;
   chain_ = comm_->ordered_collectives() && !comm_->all_local() && comm_->size() > 1;
   // CU reservation for the overlapped schedule of a real multi-rank job
   // (RCCL or its phantom): the comm / boundary / check kernels must not queue
   // behind the interior sweep, which holds every CU (LDS / VGPR file full)
   {
     int n = cfg_.reserve_cus;
-    if (const char* e = std::getenv("HEAT3D_RESERVE_CUS")) n = std::atoi(e);
     if (n < 0) n = multi_stream() && !comm_->all_local() && comm_->size() > 1 ? 8 : 0;
     if (be_->is_gpu() && n > 0) be_->reserve_cus(n);
   }
@@ -354,6 +285,7 @@ Solver::~Solver() {
   for (auto& e : cap_pool_) be_->event_destroy(e);
   for (auto& e : tev_)
     if (e) be_->event_destroy(e);
+  for (auto& e : prof_ev_) be_->event_destroy(e);
   for (auto& l : local_) {
     for (auto* f : l.field)
       if (f) be_->release(f);
@@ -370,8 +302,8 @@ Solver::~Solver() {
 // Refuses a configuration whose buffers do not fit before allocating any of
 // them: nbuf_ fields (with K-deep halos) per local rank plus the y / z face
 // staging buffers, against the backend's free memory less a reserve for RCCL
-// channels, code objects and scratch (HEAT3D_MEM_RESERVE_GB, default 2;
-// HEAT3D_MEM_PREFLIGHT=0 skips the check).  A 4096^3 fp32 grid on 2x2x2 GPUs
+// channels, code objects and scratch (--mem-reserve-gb, default 2;
+// --no-mem-preflight skips the check).  A 4096^3 fp32 grid on 2x2x2 GPUs
 // plans 3 x 34.6 GB per rank; 8192^3 fp32 on 2x2x2 (3 x 275 GB) is refused.
 void Solver::preflight_memory() {
   planned_bytes_ = 0;
@@ -390,10 +322,8 @@ void Solver::preflight_memory() {
       }
   }
   if (!be_->mem_info(&mem_free_before_, &mem_total_)) return;
-  const char* e = std::getenv("HEAT3D_MEM_PREFLIGHT");
-  if (e && e[0] == '0') return;
-  const char* rs = std::getenv("HEAT3D_MEM_RESERVE_GB");
-  const double reserve = (rs && *rs ? std::atof(rs) : 2.0) * 1e9;
+  if (!cfg_.mem_preflight) return;
+  const double reserve = cfg_.mem_reserve_gb * 1e9;
   if ((double)planned_bytes_ + reserve > (double)mem_free_before_) {
     const auto& n = cfg_.n;
     HEAT3D_THROW("memory preflight: the " << n[0] << "x" << n[1] << "x" << n[2] << " " << dtype_name(dt_)
@@ -402,7 +332,7 @@ void Solver::preflight_memory() {
                  << nbuf_ << " field buffers + face staging) plus a " << reserve / 1e9 << " GB reserve, but only "
                  << mem_free_before_ / 1e9 << " of " << mem_total_ / 1e9
                  << " GB are free; use more ranks" << (dt_ == DType::F64 ? ", fp32" : "")
-                 << (nbuf_ == 3 ? ", or two field buffers (HEAT3D_LAG=0)" : ""));
+                 << (nbuf_ == 3 ? ", or two field buffers (--lag off)" : ""));
   }
 }
 
@@ -539,6 +469,7 @@ void Solver::initialize() {
 void Solver::enqueue_halo(int p, StreamId s) {
   // p = buffer index whose faces / ghosts are exchanged
   be_->range_push("halo");
+  prof_record(prof_idx_, PE_HALO0, s);
   // one phase per axis when edges / corners must follow the faces
   // (ordered_halo_), else all faces at once
   const int nphase = ordered_halo_ ? 3 : 1;
@@ -546,6 +477,7 @@ void Solver::enqueue_halo(int p, StreamId s) {
     auto in_phase = [&](const FaceIO& io) { return !ordered_halo_ || face_axis(io.face) == ph; };
     enqueue_halo_phase(p, s, in_phase);
   }
+  prof_record(prof_idx_, PE_HALO1, s);
   be_->range_pop();
 }
 
@@ -584,6 +516,7 @@ void Solver::enqueue_halo_phase(int p, StreamId s, Pred in_phase) {
     }
     if (!xs.empty()) {
       comm_token_wait(s);
+      prof_record(prof_idx_, PE_XCHG0, s);  // first phase: the transfer may start
       comm_->exchange(xs, *be_, s);
       comm_token_signal(s);
     }
@@ -707,7 +640,7 @@ void Solver::enqueue_multi(int bi, int Kp) {
     // partial (Kp < K) or long (Kp = K + 1, single subdomain) sweep: the
     // kernel family's default variant of depth Kp
     ks = KernelSpec();
-    ks.kind = kspec2_.kind == KernelSpec::TBL ? KernelSpec::TBL : KernelSpec::TBR;
+    ks.kind = KernelSpec::TBL;
     ks.K = Kp;
   }
   // update ranges reach Kp - 1 (not K_ - 1) points into the deep halos
@@ -734,9 +667,13 @@ void Solver::enqueue_multi(int bi, int Kp) {
     ev_wait(kCompute, EV_CHK + 1);
     if (has_halo_) enqueue_halo(bi, kCompute);
     be_->range_push("sweep");
-    for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), ks, kCompute);
+    prof_record(prof_idx_, PE_INT0, kCompute);
+    for (auto& l : local_) be_->sweep(dt_, params(l, l.tb_interior), ks, kCompute);
+    prof_record(prof_idx_, PE_INT1, kCompute);
     be_->range_pop();
-    reduce_and_check(kCompute, slot0, Kp);
+    prof_record(prof_idx_, PE_RED0, kCompute);
+    reduce_and_check(kCompute, slot0, Kp, prof_idx_);
+    prof_record(prof_idx_, PE_CHK1, kCompute);
     if (!capturing_) {
       for (int i = 0; i < 2; ++i) {
         ev_record(EV_INT + i, kCompute);
@@ -754,72 +691,47 @@ void Solver::enqueue_multi(int bi, int Kp) {
   // q-1's check in both schedules' indexing; with the lag, EV_CHK + q still
   // stands for sweep q-2's (q's is recorded below).
   const int chk_prev = lag_ ? q : (q ^ 1);
+  // [B1] the deep halo of T^t first in the collective chain: it depends only
+  // on the previous sweep's boundary slabs (comm-stream order) and must not
+  // queue behind the previous sweep's all-reduce, which waits for that
+  // sweep's interior; the deferred all-reduce + check follow it.  Without the
+  // lag this sweep's interior waits for that check (chk_prev), so it is issued
+  // after the flush.
+  enqueue_halo(bi, kComm);
+  flush_pending_reduce();
   // [A] interior planes
   ev_wait(kCompute, EV_CHK + chk_prev);
   ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of our input
   be_->range_push("interior");
-  for (auto& l : local_) be_->stencil2(dt_, params(l, l.tb_interior), ks, kCompute);
+  prof_record(prof_idx_, PE_INT0, kCompute);
+  for (auto& l : local_) be_->sweep(dt_, params(l, l.tb_interior), ks, kCompute);
+  prof_record(prof_idx_, PE_INT1, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
-  // [B] deep halo, then the boundary slabs
-  enqueue_halo(bi, kComm);
-  // the previous sweep's all-reduce follows this halo in the collective
-  // chain: the halo of sweep q depends only on the boundary slabs of q-1 and
-  // must not queue behind the all-reduce of q-1, which waits for its interior
-  flush_pending_reduce();
+  // [B2] the boundary slabs, behind the halo on the comm stream
   ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
   ev_wait(kComm, EV_CHK + chk_prev);
-  // HEAT3D_BND_AFTER_INT=1: boundary slabs only after this sweep's interior
-  // (probe: with fast links they otherwise start mid-interior and take its CUs)
-  static const bool bnd_after_int = [] {
-    const char* e = std::getenv("HEAT3D_BND_AFTER_INT");
-    return e && e[0] == '1';
-  }();
-  if (bnd_after_int) ev_wait(kComm, EV_INT + q);
   be_->range_push("boundary");
+  prof_record(prof_idx_, PE_BND0, kComm);
   for (auto& l : local_) {
-    const auto& bs = l.tb_boundary;
-    std::size_t i = 0;
-    if (pair_x_slabs(bs)) {
-      // the two x slabs in one launch (StencilParams::xpair): one grid of
-      // workgroups instead of two rounds of short sweeps behind the interior
-      StencilParams sp = params(l, bs[0]);
-      sp.xpair = bs[1].lo[0] - bs[0].lo[0];
-      be_->stencil2(dt_, sp, ks, kComm);
-      i = 2;
-    }
-    for (; i < bs.size(); ++i) be_->stencil2(dt_, params(l, bs[i]), ks, kComm);
+    for (const Box& b : l.tb_boundary) be_->sweep(dt_, params(l, b), ks, kComm);
   }
+  prof_record(prof_idx_, PE_BND1, kComm);
   be_->range_pop();
   ev_record(EV_BND + q, kComm);
-  // [C] all residuals, all checks: now, or (lagged, ordered collectives) after
-  // the next sweep's halo.  Nothing waits for CHK(q) before sweep q+2 (with the
-  // lag), whose halo is issued after that point, so deferring costs nothing.
+  // [C] all residuals, all checks: now, or (ordered collectives) after the
+  // next sweep's halo.  With the lag nothing waits for CHK(q) before sweep
+  // q+2; without it sweep q+1's interior does, and is issued after the flush.
   pending_.valid = true;
   pending_.q = q;
   pending_.slot0 = slot0;
   pending_.Kp = Kp;
-  if (!(lag_ && chain_)) flush_pending_reduce();
+  pending_.prof = prof_idx_;
+  if (!chain_) flush_pending_reduce();
   ++nsweep_;
 }
 
-// The first two boundary pieces are the low and high x slabs of one shape
-// (both x faces have a neighbour): with HEAT3D_PAIR_SLABS=1 sweep them as a
-// pair (one launch of x-marching tiles).  Off by default: the phantom rank of
-// the 8-GPU bench ran 0.217 ms per step paired vs 0.213 as two launches, and
-// thin slabs now take the y-marching tiles (stencil_tbl.hip swap_xy).
-bool Solver::pair_x_slabs(const std::vector<Box>& bs) const {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT3D_PAIR_SLABS");
-    return e && e[0] == '1';
-  }();
-  if (!on || bs.size() < 2) return false;
-  const Box &a = bs[0], &b = bs[1];
-  return a.lo[1] == b.lo[1] && a.hi[1] == b.hi[1] && a.lo[2] == b.lo[2] && a.hi[2] == b.hi[2] &&
-         a.extent(0) == b.extent(0) && a.extent(0) > 0 && b.lo[0] >= a.hi[0];
-}
-
-void Solver::reduce_and_check(StreamId s, int slot0, int Kp) {
+void Solver::reduce_and_check(StreamId s, int slot0, int Kp, int prof) {
   if (!comm_->all_local() && comm_->size() > 1) {
     comm_token_wait(s);
     comm_->allreduce(&dstate_->residual[slot0], Kp, RedType::U64, RedOp::Max, *be_, s);
@@ -827,6 +739,7 @@ void Solver::reduce_and_check(StreamId s, int slot0, int Kp) {
   } else if (fake_allreduce_us_ > 0) {
     be_->delay(fake_allreduce_us_, s);  // single-GPU stand-in for the RCCL latency
   }
+  prof_record(prof, PE_REDX, s);
   be_->check_convergence(dstate_, slot0, s, Kp);
 }
 
@@ -836,8 +749,91 @@ void Solver::flush_pending_reduce() {
   const int q = pending_.q;
   ev_wait(kReduce, EV_INT + q);
   ev_wait(kReduce, EV_BND + q);
-  reduce_and_check(kReduce, pending_.slot0, pending_.Kp);
+  prof_record(pending_.prof, PE_RED0, kReduce);
+  reduce_and_check(kReduce, pending_.slot0, pending_.Kp, pending_.prof);
+  prof_record(pending_.prof, PE_CHK1, kReduce);
   ev_record(EV_CHK + q, kReduce);
+}
+
+void Solver::prof_record(int sweep, int id, StreamId s) {
+  if (!prof_on_ || sweep < 0 || capturing_) return;
+  unsigned& set = prof_set_[sweep];
+  if (set & (1u << id)) return;  // first occurrence only (e.g. the first halo phase)
+  set |= 1u << id;
+  be_->record(prof_ev_[(std::size_t)sweep * PE_COUNT + id], s);
+}
+
+std::vector<std::pair<std::string, double>> Solver::profile_sweeps(int n) {
+  std::vector<std::pair<std::string, double>> out;
+  if (!tb_ || n < 3) return out;
+  flush_pending_reduce();
+  const std::size_t need = (std::size_t)n * PE_COUNT;
+  while (prof_ev_.size() < need) prof_ev_.push_back(be_->event_create());
+  prof_set_.assign(n, 0u);
+  prof_on_ = true;
+  try {
+    for (int i = 0; i < n; ++i) {
+      prof_idx_ = i;
+      record_segment(issued_, K_, cur());
+      enqueue_multi(cur(), K_);
+      issued_ += K_;
+      cur_ = nxt(cur_);
+    }
+    prof_idx_ = -1;
+    flush_pending_reduce();
+    be_->sync_all();
+  } catch (...) {
+    prof_on_ = false;
+    prof_idx_ = -1;
+    throw;
+  }
+  prof_on_ = false;
+  comm_->check_async_error();
+  auto ev = [&](int i, int id) { return prof_ev_[(std::size_t)i * PE_COUNT + id]; };
+  auto has = [&](int i, int id) { return (prof_set_[i] >> id) & 1u; };
+  auto ms = [&](int i, int a, int j, int b) { return (double)be_->elapsed_ms(ev(i, a), ev(j, b)); };
+  // sweeps 1 .. n-2: every one has a predecessor and a successor in the window
+  std::map<std::string, std::pair<double, int>> acc;
+  auto add = [&](const char* k, double v) {
+    auto& a = acc[k];
+    a.first += v;
+    a.second += 1;
+  };
+  for (int i = 1; i + 1 < n; ++i) {
+    if (!has(i, PE_INT0) || !has(i, PE_INT1)) continue;
+    add("interior_ms", ms(i, PE_INT0, i, PE_INT1));
+    add("sweep_ms", ms(i, PE_INT0, i + 1, PE_INT0));
+    add("compute_idle_ms", ms(i, PE_INT1, i + 1, PE_INT0));
+    if (has(i, PE_HALO0) && has(i, PE_HALO1)) {
+      add("halo_ms", ms(i, PE_HALO0, i, PE_HALO1));
+      if (has(i, PE_XCHG0)) {
+        add("halo_token_wait_ms", ms(i, PE_HALO0, i, PE_XCHG0));
+        add("halo_transfer_ms", ms(i, PE_XCHG0, i, PE_HALO1));
+      }
+    }
+    if (has(i, PE_BND0) && has(i, PE_BND1)) {
+      add("boundary_ms", ms(i, PE_BND0, i, PE_BND1));
+      if (has(i, PE_HALO1)) add("boundary_wait_ms", ms(i, PE_HALO1, i, PE_BND0));
+      // boundary chain end relative to the interior's end (> 0: exposed tail)
+      add("boundary_tail_ms", ms(i, PE_INT1, i, PE_BND1));
+      if (has(i, PE_HALO0)) {
+        // overlap of [halo start, boundary end] with [interior start, end]
+        const double c0 = ms(i, PE_INT0, i, PE_HALO0), c1 = ms(i, PE_INT0, i, PE_BND1);
+        const double e = ms(i, PE_INT0, i, PE_INT1);
+        const double lo = std::max(0.0, c0), hi = std::min(e, c1);
+        add("chain_overlap_fraction", c1 > c0 ? std::max(0.0, hi - lo) / (c1 - c0) : 0.0);
+        add("halo_start_after_interior_start_ms", c0);
+      }
+    }
+    if (has(i, PE_RED0) && has(i, PE_REDX) && has(i, PE_CHK1)) {
+      add("allreduce_ms", ms(i, PE_RED0, i, PE_REDX));
+      add("check_ms", ms(i, PE_REDX, i, PE_CHK1));
+    }
+  }
+  out.push_back({"sweeps", (double)(n - 2)});
+  out.push_back({"steps_per_sweep", (double)K_});
+  for (auto& kv : acc) out.push_back({kv.first, kv.second.first / std::max(1, kv.second.second)});
+  return out;
 }
 
 void Solver::comm_token_wait(StreamId s) {
@@ -939,26 +935,24 @@ int Solver::long_sweeps_for(int64_t n) const {
   if (K_ + 1 > 6 || K_ + 1 > kResidualSlots) return 0;
   const int64_t b = n % K_;             // n = a K + b (K + 1) with a = (n - b (K + 1)) / K
   if (b * (K_ + 1) > n) return 0;
-  static const bool off = [] {
-    const char* e = std::getenv("HEAT3D_LONG_SWEEPS");
-    return e && e[0] == '0';
-  }();
-  return off ? 0 : (int)b;
+  if (!cfg_.long_sweeps) return 0;
+  // the K+1 variant must exist for this dtype (e.g. fp64 K = 5 has no K = 6)
+  KernelSpec ks;
+  ks.kind = KernelSpec::TBL;
+  ks.K = K_ + 1;
+  return be_->is_gpu() && !hip::lean_supported(dt_, ks) ? 0 : (int)b;
 }
 
 bool Solver::graphs_allowed() const {
   // Multi-stream (overlapped) schedules can be graphs too (built explicitly by
   // the backend's recorder, bitwise equal to eager runs: tests/test_gpu_graph.py),
-  // but only with HEAT3D_GRAPH_MULTISTREAM=1: the HIP runtime replays the
+  // but only with --graph-multistream: the HIP runtime replays the
   // graph's parallel branches without stream priorities, so the boundary
   // slabs and halo copies compete with the interior sweep (phantom rank of the
   // 8-GPU bench: 0.28 ms/step as a graph, 0.21 eager; profiles/rank_proxy_r02.md)
   // and the overlapped schedule runs eagerly — its host cost is far below its
   // GPU time at these sizes.
-  static const bool ms_ok = [] {
-    const char* e = std::getenv("HEAT3D_GRAPH_MULTISTREAM");
-    return e && e[0] == '1';
-  }();
+  const bool ms_ok = cfg_.graph_multistream;
   return cfg_.use_graph && be_->supports_graphs() && comm_->capturable() && !graph_failed_ && !phase_timing_ &&
          (!multi_stream() || ms_ok);
 }
@@ -1180,7 +1174,7 @@ RunResult Solver::run() {
   int64_t next_verify = cfg_.verify_halo > 0 ? issued_ + cfg_.verify_halo : -1;
   if (cfg_.timers) set_phase_timing(true);
   int64_t printed = issued_;
-  const double watchdog = std::getenv("HEAT3D_WATCHDOG_S") ? std::atof(std::getenv("HEAT3D_WATCHDOG_S")) : 900.0;
+  const double watchdog = cfg_.watchdog_s;
   while (issued_ < cfg_.iter_max && !stop) {
     int64_t n = std::min(K, cfg_.iter_max - issued_);
     if (next_ckpt > 0) n = std::min(n, next_ckpt - issued_);
@@ -1300,29 +1294,26 @@ std::vector<double> Solver::local_field(int idx, bool with_ghosts) {
 }
 
 // Host memory a root-side gather may use: half of the physical RAM, unless
-// HEAT3D_HOST_MEM_LIMIT_GB says otherwise.
-static double host_mem_limit_bytes() {
-  if (const char* e = std::getenv("HEAT3D_HOST_MEM_LIMIT_GB")) return std::atof(e) * 1e9;
+// --host-mem-limit-gb says otherwise.
+static double host_mem_limit_bytes(const Config& c) {
+  if (c.host_mem_limit_gb > 0) return c.host_mem_limit_gb * 1e9;
   const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
   return pages > 0 && psz > 0 ? 0.5 * (double)pages * (double)psz : 64e9;
 }
 
 // Staging chunk of the streamed I/O paths (device stage + pinned host buffer).
-static std::size_t io_stage_bytes() {
-  if (const char* e = std::getenv("HEAT3D_IO_STAGE_MB")) return std::max<std::size_t>(1, std::atoll(e)) << 20;
-  return (std::size_t)64 << 20;
-}
+static std::size_t io_stage_bytes(const Config& c) { return (std::size_t)std::max(1, c.io_stage_mb) << 20; }
 
 // Visit the box `g` (global coords) of local subdomain `l` in x chunks of at
-// most io_stage_bytes(): pack the chunk on the device, copy it to pinned host
+// most stage_bytes: pack the chunk on the device, copy it to pinned host
 // memory and call fn(x0, nx, host) with nx planes of g.extent(1) x
 // g.extent(2) values (z fastest).  Memory stays bounded by one chunk.
 template <typename Fn>
 static void stream_box_out(Backend& be, DType dt, std::size_t esize, const void* field, const Layout& L,
-                           const Subdomain& sd, const Box& g, Fn fn) {
+                           const Subdomain& sd, const Box& g, std::size_t stage_bytes, Fn fn) {
   const int64_t plane = g.extent(1) * g.extent(2);
   if (plane <= 0 || g.extent(0) <= 0) return;
-  const int64_t xc = std::max<int64_t>(1, std::min<int64_t>(g.extent(0), io_stage_bytes() / (plane * esize)));
+  const int64_t xc = std::max<int64_t>(1, std::min<int64_t>(g.extent(0), (int64_t)stage_bytes / (plane * esize)));
   void* stage = be.alloc(xc * plane * esize);
   void* host = be.alloc_host(xc * plane * esize);
   try {
@@ -1356,12 +1347,12 @@ bool Solver::gather_global(std::vector<double>* out) {
   const int p = cur();
   const int64_t* N = dec_.N;
   const double need = 8.0 * (double)N[0] * (double)N[1] * (double)N[2];
-  const bool ok = need <= host_mem_limit_bytes();
+  const bool ok = need <= host_mem_limit_bytes(cfg_);
   if (!ok) {
     // every rank throws (same test): no rank is left waiting in a send
     HEAT3D_THROW("gathering the " << N[0] << "x" << N[1] << "x" << N[2] << " field on the root needs " << need / 1e9
-                                  << " GB of host memory (limit " << host_mem_limit_bytes() / 1e9
-                                  << " GB, HEAT3D_HOST_MEM_LIMIT_GB); write per-rank Tecplot zones "
+                                  << " GB of host memory (limit " << host_mem_limit_bytes(cfg_) / 1e9
+                                  << " GB, --host-mem-limit-gb); write per-rank Tecplot zones "
                                      "(--tecplot-layout owned) or a checkpoint instead");
   }
   if (root) out->assign((std::size_t)(N[0] * N[1] * N[2]), 0.0);
@@ -1390,7 +1381,7 @@ bool Solver::gather_global(std::vector<double>* out) {
     if (li >= 0 && root) {
       // the root's own blocks: streamed, no full-block stage
       Local& l = local_[li];
-      stream_box_out(*be_, dt_, esize_, l.field[p], l.L, l.sd, g, [&](int64_t x0, int64_t nx, const char* h) {
+      stream_box_out(*be_, dt_, esize_, l.field[p], l.L, l.sd, g, io_stage_bytes(cfg_), [&](int64_t x0, int64_t nx, const char* h) {
         Box c = g;
         c.lo[0] = g.lo[0] + x0;
         c.hi[0] = c.lo[0] + nx;
@@ -1511,7 +1502,7 @@ void Solver::write_tecplot_zones(const std::string& path) {
     const int64_t body = off[r] + (int64_t)zh.size();
     const int64_t ex = g.extent(0), ey = g.extent(1), ez = g.extent(2);
     // the zone runs k outermost, i innermost: stream z chunks of the box
-    const int64_t kc = std::max<int64_t>(1, std::min<int64_t>(ez, io_stage_bytes() / std::max<int64_t>(1, ex * ey * esize_)));
+    const int64_t kc = std::max<int64_t>(1, std::min<int64_t>(ez, io_stage_bytes(cfg_) / std::max<int64_t>(1, ex * ey * esize_)));
     void* stage = be_->alloc(ex * ey * kc * esize_);
     std::vector<char> host(ex * ey * kc * esize_);
     std::string text;
@@ -1612,7 +1603,7 @@ void Solver::save_checkpoint(const std::string& dir) {
     for (auto& l : local_) {
       const Box g = l.sd.extended_global();
       const int64_t ey = g.extent(1), ez = g.extent(2);
-      stream_box_out(*be_, dt_, esize_, l.field[p], l.L, l.sd, g, [&](int64_t x0, int64_t nx, const char* h) {
+      stream_box_out(*be_, dt_, esize_, l.field[p], l.L, l.sd, g, io_stage_bytes(cfg_), [&](int64_t x0, int64_t nx, const char* h) {
         sum += host_bitsum(h, nx * ey * ez, dt_);
         for (int64_t i = 0; i < nx; ++i) {
           const int64_t gi = g.lo[0] + x0 + i;
@@ -1687,7 +1678,7 @@ void Solver::load_checkpoint(const std::string& dir) {
     }
     const Box ext = l.sd.extended_global();
     const int64_t ey = lb.extent(1), ez = lb.extent(2), plane = ey * ez;
-    const int64_t xc = std::max<int64_t>(1, std::min<int64_t>(lb.extent(0), io_stage_bytes() / (plane * esize_)));
+    const int64_t xc = std::max<int64_t>(1, std::min<int64_t>(lb.extent(0), io_stage_bytes(cfg_) / (plane * esize_)));
     std::vector<char> host(xc * plane * esize_);
     void* stage = be_->alloc(host.size());
     for (int64_t x0 = 0; x0 < lb.extent(0); x0 += xc) {
@@ -1884,12 +1875,12 @@ std::unique_ptr<Solver> make_solver(const Config& cfg, const RankPlacement& w) {
     case CommKind::Rccl: {
       HEAT3D_CHECK(bk == BackendKind::Hip, "RCCL needs the HIP backend");
       if (!w.rccl_uid.empty()) {
-        comm = make_rccl_comm(rank, size, w.rccl_uid, device);
+        comm = make_rccl_comm(rank, size, w.rccl_uid, device, rccl_options(cfg));
       } else {
         net::Bootstrap boot(rank, size, master, bport);
         std::string uid = rank == 0 ? rccl_unique_id() : std::string();
         auto all = boot.allgather(uid);
-        comm = make_rccl_comm(rank, size, all[0], device);
+        comm = make_rccl_comm(rank, size, all[0], device, rccl_options(cfg));
       }
       nranks = size;
       break;

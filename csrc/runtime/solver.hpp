@@ -142,6 +142,16 @@ class Solver {
   }
   std::vector<std::pair<std::string, double>> phase_times();
 
+  // Schedule profile of the production sweep pipeline (diagnostic, run it
+  // outside any timed window): issues n more temporally blocked sweeps eagerly
+  // with timing events at the phase boundaries of every stream and returns
+  // per-sweep means in ms (interior, halo, boundary, all-reduce, check, sweep
+  // period, compute-stream idle, boundary tail after the interior) plus the
+  // fraction of the halo + boundary chain that ran while the interior did.
+  // Unlike set_phase_timing() nothing is synchronised between sweeps, so the
+  // numbers describe the overlapped schedule as it runs.
+  std::vector<std::pair<std::string, double>> profile_sweeps(int n);
+
   // Race detection: compare order-independent checksums of every face sent
   // in the last exchange with the ghost layer the neighbour received.
   // Returns the number of mismatching faces (0 = consistent).
@@ -193,8 +203,7 @@ class Solver {
   void comm_token_wait(StreamId s);
   void comm_token_signal(StreamId s);
   // all-reduce + check of one sweep (residual slots slot0 .. slot0+Kp-1)
-  void reduce_and_check(StreamId s, int slot0, int Kp);
-  bool pair_x_slabs(const std::vector<Box>& bs) const;
+  void reduce_and_check(StreamId s, int slot0, int Kp, int prof = -1);
   // lagged overlapped sweeps: the all-reduce of sweep q is issued after the
   // halo of sweep q+1 (see enqueue_multi); flush issues a pending one
   void flush_pending_reduce();
@@ -276,6 +285,7 @@ class Solver {
   struct PendingReduce {
     bool valid = false;
     int q = 0, slot0 = 0, Kp = 0;
+    int prof = -1;  // profiled sweep index (profile_sweeps)
   } pending_;
   Event ev_[EV_COUNT] = {};
   Event cur_ev_[EV_COUNT] = {};     // event currently standing for each id
@@ -293,6 +303,14 @@ class Solver {
   int64_t phase_count_ = 0;
   Event tev_[8] = {};
   void accumulate_phase_times();
+
+  // profile_sweeps: events per profiled sweep, recorded only while prof_on_
+  enum { PE_INT0, PE_INT1, PE_HALO0, PE_XCHG0, PE_HALO1, PE_BND0, PE_BND1, PE_RED0, PE_REDX, PE_CHK1, PE_COUNT };
+  bool prof_on_ = false;
+  int prof_idx_ = -1;                 // sweep being issued
+  std::vector<Event> prof_ev_;        // PE_COUNT per sweep
+  std::vector<unsigned> prof_set_;    // bit mask of the events recorded per sweep
+  void prof_record(int sweep, int id, StreamId s);
 };
 
 // Where one rank of a job runs: its rank, the job size, the GPU it binds, and
@@ -307,6 +325,22 @@ struct RankPlacement {
   int bootstrap_port = 29501;
   std::string rccl_uid;
 };
+
+// Communicator options from the run configuration
+inline RcclOptions rccl_options(const Config& c) {
+  RcclOptions o;
+  o.shared = c.rccl_shared;
+  o.graph = c.rccl_graph;
+  return o;
+}
+inline PhantomOptions phantom_options(const Config& c) {
+  PhantomOptions o;
+  o.gbps = c.phantom_gbps;
+  o.allreduce_us = c.phantom_allreduce_us;
+  o.channels = c.phantom_channels;
+  o.allreduce_channels = c.phantom_allreduce_channels;
+  return o;
+}
 
 // Build a Solver for one rank: chooses backend, comm (RCCL / socket through
 // the bootstrap, LocalComm for --virtual-ranks), decomposition.

@@ -107,12 +107,11 @@ def ftcs_step2(src: PaddedField, dst: PaddedField, D: Sequence[float], kernel: s
                state: Optional[torch.Tensor] = None, slot: int = 0) -> None:
     """dst = K FTCS steps of src in ONE temporally blocked sweep (gfx950).
 
-    ``kernel`` picks the depth: ``tb2[:V:R:WZ:WY:L]`` (tuned 2-step kernel,
-    the default), ``tb3`` .. ``tb6`` or ``tbk2`` (generic K-step kernel,
-    stencil_tbk.hip).  The ghost shell of ``src`` is treated as constant
-    (Dirichlet) for every step; the residual of step s lands in ``state``
-    slot ``slot + s`` (tb2: ``slot`` and ``slot ^ 1``).  Bitwise identical to
-    K ``ftcs_step`` calls.
+    ``kernel`` picks the depth and variant: ``tl2`` .. ``tl6[:V:R:WZ:WY:L:Q]``
+    (the lean K-step kernel, stencil_tbl.hip / stencil_tbp.hip); ``auto`` is
+    ``tl2``.  The ghost shell of ``src`` is treated as constant (Dirichlet)
+    for every step; the residual of step s lands in ``state`` slot
+    ``slot + s``.  Bitwise identical to K ``ftcs_step`` calls.
     """
     if src.layout != dst.layout or src.dtype != dst.dtype or src.device != dst.device:
         raise ValueError("src and dst must share layout, dtype and device")
@@ -128,22 +127,13 @@ def ftcs_step2(src: PaddedField, dst: PaddedField, D: Sequence[float], kernel: s
 
 
 def sweep(src: PaddedField, dst: PaddedField, D: Sequence[float], box: Sequence[int],
-          ux: Sequence[int] = (0, -1), kernel: str = "tb3", state: Optional[torch.Tensor] = None,
-          slot: int = 0, xpair: int = 0) -> None:
-    """One K-step sweep (K from ``kernel``: tb2, tbk2, tb3..tb6) on ``box``
+          ux: Sequence[int] = (0, -1), kernel: str = "tl3", state: Optional[torch.Tensor] = None,
+          slot: int = 0) -> None:
+    """One K-step sweep (K from ``kernel``: tl2..tl6) on ``box``
     = (x0, x1, y0, y1, z0, z1) of a deep-ghost field, with the intermediate
     steps computed on the x range ``ux`` (the solver's x-slab schedule).
-    ``xpair`` > 0 also sweeps the box shifted by ``xpair`` along x (the two
-    boundary slabs of an x slab; one launch for the fp64 lean kernel).
     GPU tensors run the gfx950 kernel, CPU tensors the K-single-steps
     definition (csrc/kernels/kernels_cpu.cpp)."""
-    if xpair and src.device.type != "cuda":
-        sweep(src, dst, D, box, ux, kernel, state, slot)
-        b = list(box)
-        b[0] += xpair
-        b[1] += xpair
-        sweep(src, dst, D, b, ux, kernel, state, slot)
-        return
     if src.layout != dst.layout or src.dtype != dst.dtype or src.device != dst.device:
         raise ValueError("src and dst must share layout, dtype and device")
     sptr = 0
@@ -154,19 +144,16 @@ def sweep(src: PaddedField, dst: PaddedField, D: Sequence[float], box: Sequence[
     args = (src.dt, src.data_ptr(), dst.data_ptr(), list(src.n), src.gx, list(box), list(ux), list(D), sptr, slot,
             kernel)
     if src.device.type == "cuda":
-        if xpair:
-            native().hip.stencil_sweep_xpair(*args, xpair, _stream_ptr(src.flat))
-        else:
-            native().hip.stencil_sweep(*args, _stream_ptr(src.flat))
+        native().hip.stencil_sweep(*args, _stream_ptr(src.flat))
     else:
         native().cpu.stencil_sweep(*args)
 
 
 def sweep3(src: PaddedField, dst: PaddedField, D: Sequence[float], box: Sequence[int], u: Sequence[int],
-           kernel: str = "tr3", state: Optional[torch.Tensor] = None, slot: int = 0) -> None:
+           kernel: str = "tl3", state: Optional[torch.Tensor] = None, slot: int = 0) -> None:
     """K-step sweep with deep ghosts on every axis (the block-decomposition
     schedule): ``u`` = (ux0, ux1, uy0, uy1, uz0, uz1) are the update ranges of
-    the intermediate steps.  GPU tensors run the ring kernel, CPU tensors the
+    the intermediate steps.  GPU tensors run the lean kernel, CPU tensors the
     K-single-steps definition."""
     if src.layout != dst.layout or src.dtype != dst.dtype or src.device != dst.device:
         raise ValueError("src and dst must share layout, dtype and device")

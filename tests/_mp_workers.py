@@ -114,7 +114,7 @@ def native_staged_cpu_worker(rank, world, port, outdir, n, eps, decomp, extra_ar
     dist.destroy_process_group()
 
 
-def native_rccl_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, extra_args=(), env=None):
+def native_rccl_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, extra_args=()):
     """Native engine, HIP backend, a real multi-rank RCCL communicator with all
     ranks on the one visible GPU: every rank gets its own NCCL_HOSTID, so RCCL
     accepts the shared device (it refuses two ranks per GPU of one host) and
@@ -122,8 +122,6 @@ def native_rccl_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, ext
     RcclComm::exchange (ncclSend / ncclRecv groups with real peers) and the
     all-reduce of the residual slots through the production schedule."""
     os.environ.update({"NCCL_HOSTID": f"heat3d-test-rank{rank}", "NCCL_SOCKET_IFNAME": "lo"})
-    if env:
-        os.environ.update(env)
     dist = _init(rank, world, port)
     import heat3d_amd
 

@@ -53,13 +53,12 @@ def test_cli_two_processes_one_gpu(heat3d_bin, gpu, tmp_path):
 
 
 @pytest.mark.parametrize("rank,size,decomp", [(1, 4, (4, 1, 1)), (5, 8, (2, 2, 2))])
-def test_phantom_rank_gpu(h3d, gpu, rank, size, decomp, monkeypatch):
+def test_phantom_rank_gpu(h3d, gpu, rank, size, decomp):
     """PhantomComm on the GPU (tools/rank_proxy.py): one rank's full overlapped
     schedule with emulated halo delay kernels; every issued iteration checked."""
-    monkeypatch.setenv("HEAT3D_PHANTOM_GBPS", "50")
-    monkeypatch.setenv("HEAT3D_PHANTOM_ALLREDUCE_US", "5")
     s = h3d.HeatSolver((97, 97, 97), 1 << 40, 0.0, backend="hip", device=0, decomp=decomp,
-                       phantom=(rank, size), extra_args=["--temporal", "3"])
+                       phantom=(rank, size), extra_args=["--temporal", "3", "--phantom-gbps", "50",
+                                                         "--phantom-allreduce-us", "5"])
     assert s.native.comm_name == "phantom"
     s.initialize()
     s.step(40)

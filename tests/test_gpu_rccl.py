@@ -38,21 +38,21 @@ def test_rccl_self_exchange(ext, gpu):
     assert r["allreduce_f64"] == (1.5, -2.25)
 
 
-@pytest.mark.parametrize("world,decomp,env", [
+@pytest.mark.parametrize("world,decomp,extra", [
     (2, (2, 1, 1), None),
-    (2, (2, 1, 1), {"HEAT3D_RCCL_SHARED": "1"}),     # one communicator for halos and all-reduce
+    (2, (2, 1, 1), ["--rccl-shared"]),               # one communicator for halos and all-reduce
     (4, (2, 2, 1), None),                             # block: deep y halos, axis-ordered phases
 ])
-def test_rccl_multirank_bitwise(h3d, gpu, tmp_path, world, decomp, env):
+def test_rccl_multirank_bitwise(h3d, gpu, tmp_path, world, decomp, extra):
     n, eps = 33, 1e-4
     mp.start_processes(native_rccl_gpu_worker,
-                       args=(world, free_port(), str(tmp_path), n, eps, decomp, "fp64", [], env),
+                       args=(world, free_port(), str(tmp_path), n, eps, decomp, "fp64", extra or []),
                        nprocs=world, join=True, start_method="spawn")
     single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="hip", device=0)
     r1 = single.run()
     it, err, name, graphs = open(tmp_path / "result.txt").read().split()
     assert int(it) == r1["conv_iter"]  # the same stopping iteration as one rank
-    assert name == ("rccl(shared)" if env else "rccl")
+    assert name == ("rccl(shared)" if extra else "rccl")
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
 
 
@@ -85,3 +85,23 @@ def test_bench_self_launch_socket(gpu, tmp_path):
     j = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
     assert j["n_gpus"] == 2 and j["comm_ranks"] == 2 and j["config"]["comm"] == "staged-socket"
     assert j["metric"].endswith("128^3 fp64 grid") and j["config"]["model"].endswith("128^3 fp64 grid")
+
+
+@pytest.mark.parametrize("world,decomp", [(2, (2, 1, 1)), (4, (2, 2, 1))])
+def test_rccl_graph_bitwise(h3d, gpu, tmp_path, world, decomp):
+    """RCCL send / recv groups and all-reduces recorded into hipGraphs
+    (--rccl-graph, single-stream schedule): the ranks replay graphs
+    (graph_launches > 0), exit cleanly and give the field of the eager
+    single-process solve bit for bit.  Reference per-iteration comm:
+    heat3D.cu:619-641 (halo), 1062-1063 (reduction)."""
+    n, eps = 33, 1e-4
+    extra = ["--no-overlap", "--rccl-graph", "--watchdog", "60"]
+    mp.start_processes(native_rccl_gpu_worker,
+                       args=(world, free_port(), str(tmp_path), n, eps, decomp, "fp64", extra),
+                       nprocs=world, join=True, start_method="spawn")
+    single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="hip", device=0, graph=False)
+    r1 = single.run()
+    it, err, name, graphs = open(tmp_path / "result.txt").read().split()
+    assert int(graphs) > 0, "no hipGraph was replayed"
+    assert int(it) == r1["conv_iter"] and name == "rccl"
+    assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())

@@ -98,7 +98,7 @@ def test_schedules_bitwise(h3d, gpu, graph, overlap):
     assert np.array_equal(s.gather(), base.gather())
 
 
-@pytest.mark.parametrize("kernel", ["naive", "column:2:4", "column:2:8", "column:1:8"])
+@pytest.mark.parametrize("kernel", ["naive", "tile", "tile:2:4:2:4"])
 def test_kernel_variants_solver(h3d, gpu, kernel):
     s, r = _solve(h3d, 64, 1e-3, kernel=kernel)
     assert r["conv_iter"] == 1915

@@ -1,15 +1,15 @@
-"""2-step temporally blocked gfx950 kernel (stencil_tb2.hip) and the solver's
-double-step schedule: bitwise identical to two single steps / to the
-single-step solver, including convergence in the first half of a pair."""
+"""K-step temporally blocked gfx950 sweeps (the lean kernel stencil_tbl.hip and
+its packed fp32 pair form stencil_tbp.hip) and the solver's sweep schedules:
+bitwise identical to K single steps / to the single-step solver, all K
+residuals included, convergence inside a sweep rolled back exactly."""
 import numpy as np
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS_F64 = ["tb2", "tb2:2:2:1:8", "tb2:2:2:1:16", "tb2:2:3:1:4", "tb2:2:4:2:4", "tb2:2:4:4:2", "tb2:2:4:1:4", "tb2:2:4:2:2", "tb2:2:8:2:2",
-                "tb2:2:4:2:4:5", "tb2:2:4:2:4:1", "tb2:2:2:2:8"]
-VARIANTS_F32 = ["tb2", "tb2:4:2:1:8", "tb2:4:3:1:4", "tb2:4:4:2:4", "tb2:4:4:2:2", "tb2:2:4:2:4", "tb2:4:4:2:4:3"]
+VARIANTS_F64 = ["auto", "tl2", "tl2:1:2:1:16:0:3", "tl2:1:3:1:16:0:3", "tl2:1:2:1:16:0:6", "tl2:1:2:1:16:5:3"]
+VARIANTS_F32 = ["auto", "tl2", "tl2:2:2:1:16:0:3", "tl2:2:3:1:16:0:3", "tl2:1:3:1:16:0:3", "tl2:1:2:1:16:0:6"]
 
 
 def _field(ops, n, dtype, gpu, seed):
@@ -103,26 +103,17 @@ def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
     assert np.array_equal(a.gather(), b.gather())
 
 
-VARIANTS_K = {3: ["tb3", "tb3:1:4:1:16:0:1", "tb3:1:4:1:16:0:3", "tb3:1:3:1:16", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb3:1:4:1:16", "tb3:1:6:1:8", "tb3:1:4:2:8", "tb3:1:4:1:8:3",
-                  "tr3", "tr3:1:3:1:16:0:3", "tr3:1:4:1:8:0:4", "tr3:1:6:1:8:0:3", "tr3:1:4:1:8:5:3", "tr3:1:2:1:16:0:3",
-                  "tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5:3", "tl3:1:3:1:16:0:6",
+VARIANTS_K = {3: ["tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5:3", "tl3:1:3:1:16:0:6",
                   "tl3:1:2:1:16:7:6", "tl3:1:6:1:8:0:3", "tl3:1:3:1:16:0:3:2", "tl3:1:3:1:16:0:3:19", "tl3:1:3:1:16:0:3:0"],
-              4: ["tb4", "tb4:1:6:1:8", "tb4:1:4:1:8:1", "tr4", "tr4:1:4:1:8:0:3", "tr4:1:4:1:8:0:4",
-                  "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6",
+              4: ["tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6",
                   "tl4:1:6:1:8:0:3", "tl4:1:6:1:8:0:4", "tl4:1:5:1:8:0:3", "tl4:1:6:1:8:7:3",
                   "tl4:1:3:1:12:0:3:2", "tl4:1:3:1:12:0:3"],
-              2: ["tbk2", "tbk2:2:2:1:8", "tr2", "tr2:2:2:1:8:0:3", "tr2:1:4:1:16:0:3", "tr2:1:2:1:16",
-                  "tl2", "tl2:1:2:1:16:0:3"]}
+              2: ["tl2", "tl2:1:2:1:16:0:3"]}
 # fp32 only: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)
 PAIR = {3: ["tl3:2:3:1:16:0:3", "tl3:2:3:1:16:0:3:2", "tl3:2:3:1:16:0:4", "tl3:2:2:1:16:0:3", "tl3:2:3:1:16:5:3"],
         4: ["tl4:2:2:1:16:0:3", "tl4:2:2:1:16:0:4", "tl4:2:2:1:16:7:3"],
         2: ["tl2:2:2:1:16:0:3", "tl2:2:3:1:16:0:3"]}
-# round-1 ring-kernel variants that spill registers in fp32 since the residual
-# is taken in the field's precision (launch refuses them; tools/kres.sh)
-TBR_F32_SPILL = {"tr3:1:2:1:16:0:3", "tr3:2:4:1:8:0:4", "tr4:2:4:1:8:0:4", "tr3:2:4:1:16:0:3"}
-VARIANTS_K_F32 = {3: ["tr3:2:4:1:8:0:3"] + PAIR[3],
-                  4: PAIR[4],
-                  2: ["tr2:2:4:1:8:0:3"] + PAIR[2]}  # tr2:2:4:1:8:0:4 spills since the fp32 residual
+VARIANTS_K_F32 = PAIR
 
 
 @pytest.mark.parametrize("K", [2, 3, 4])
@@ -141,8 +132,6 @@ def test_stencil_k_bitwise(h3d, gpu, K, dtype, n):
         refs.append(r)
     want = T[1:-1, 1:-1, 1:-1]
     for v in VARIANTS_K[K] + (VARIANTS_K_F32[K] if dtype == torch.float32 else []):
-        if dtype == torch.float32 and v in TBR_F32_SPILL:
-            continue
         out = ops.PaddedField(n, dtype=dtype, device=gpu)
         out.flat.fill_(-3.0)
         st = ops.new_state(gpu)
@@ -182,9 +171,7 @@ def _deep_random(ops, n, gx, dtype, seed):
     return f
 
 
-@pytest.mark.parametrize("kernel", ["tb2", "tbk2", "tb3", "tb3:1:4:1:8", "tb3:2:2:1:8", "tb4", "tb4:1:6:1:8",
-                                    "tr2", "tr3", "tr3:1:3:1:16:0:3", "tr4", "tr2:2:2:1:8:0:3",
-                                    "tl2", "tl3", "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:0:6",
+@pytest.mark.parametrize("kernel", ["tl2", "tl3", "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:0:6",
                                     "tl4:1:6:1:8:0:3", "tl3:1:6:1:8:0:3"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (5, (0, 5), "lo"), (9, (0, 9), "hi"),
@@ -204,72 +191,22 @@ def test_sweep_pair_deep_halo_matches_cpu(h3d, gpu, kernel, n0, box_x, side):
     _deep_halo_case(h3d, gpu, kernel, torch.float32, n0, box_x, side)
 
 
-@pytest.mark.parametrize("kernel,dtype", [("tl3", torch.float64), ("tl4", torch.float64), ("tl2", torch.float64),
-                                          ("tl3:1:3:1:16:0:3:0", torch.float64), ("tl3", torch.float32),
-                                          ("tr3", torch.float64)])
-@pytest.mark.parametrize("n0,thick", [(30, 3), (9, 3), (6, 3), (130, 3), (12, 4)])
-def test_sweep_xpair_matches_cpu(h3d, gpu, kernel, dtype, n0, thick):
-    """Both boundary slabs of an x slab in one launch (StencilParams::xpair):
-    equal to the two slabs swept separately by the CPU definition, residuals
-    included."""
-    ops = h3d.ops
-    head = kernel.split(":")[0]
-    K = int(head[2])
-    if thick < K or 2 * thick > n0:
-        pytest.skip("slabs thinner than K or overlapping")
-    n = (n0, 37, 133)
-    ux = (-(K - 1), n0 + K - 1)
-    box = (0, thick, 0, n[1], 0, n[2])
-    xpair = n0 - thick
-    D = (0.06, 0.05, 0.04)
-    src = _deep_random(ops, n, K, dtype, 11)
-    want = ops.PaddedField(n, dtype=dtype, gx=K)
-    want.flat.fill_(-5.0)
-    st_c = ops.new_state("cpu")
-    ops.sweep(src, want, D, box, ux, kernel=kernel, state=st_c, xpair=xpair)
-    dsrc = ops.PaddedField(n, dtype=dtype, device=gpu, gx=K)
-    dsrc.flat.copy_(src.flat)
-    got = ops.PaddedField(n, dtype=dtype, device=gpu, gx=K)
-    got.flat.fill_(-5.0)
-    st_g = ops.new_state(gpu)
-    ops.sweep(dsrc, got, D, box, ux, kernel=kernel, state=st_g, xpair=xpair)
-    torch.cuda.synchronize()
-    g, w = got.owned().cpu(), want.owned()
-    for x0, x1 in ((0, thick), (xpair, n0)):
-        assert torch.equal(g[x0:x1], w[x0:x1]), f"{kernel} {n0} slab {x0}: max diff {(g[x0:x1] - w[x0:x1]).abs().max().item()}"
-    assert torch.equal(g[thick:xpair], torch.full_like(g[thick:xpair], -5.0)), "wrote between the slabs"
-    for s in range(K):
-        assert ops.residual_from_state(st_g, s) == ops.residual_from_state(st_c, s), (kernel, s)
-
-
 @pytest.mark.parametrize("kernel", ["tl3", "tl3:1:3:1:16:0:3"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("n0,box_x,side,ny", [(12, (0, 3), "both", 64), (12, (9, 12), "both", 64),
                                                (6, (0, 3), "lo", 100), (9, (6, 9), "hi", 49),
                                                (20, (0, 4), "both", 70), (8, (0, 6), "both", 130)])
 def test_sweep_thin_slab_y_marching(h3d, gpu, kernel, dtype, n0, box_x, side, ny):
-    """Thin x slabs with a long y extent take the y-marching tiles with
-    HEAT3D_TL_SWAP=1 (the default tl3 spec; the explicit shape stays
-    x-marching): both equal the CPU K-single-steps definition.  The switch is
-    read once per process, so this runs in a child process."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    root = os.path.dirname(here)
-    code = (f"import sys; sys.path[:0] = [{root!r}, {here!r}]; import torch, heat3d_amd as h3d; "
-            f"from test_gpu_temporal import _deep_halo_case; "
-            f"_deep_halo_case(h3d, torch.device('cuda', 0), {kernel!r}, torch.{str(dtype).split('.')[-1]}, "
-            f"{n0}, {box_x!r}, {side!r}, {ny})")
-    env = dict(os.environ, HEAT3D_TL_SWAP="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=100)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    """Thin x slabs with a long y extent take the y-marching tiles (the
+    default tl3 spec; an explicit shape stays x-marching): both equal the CPU
+    K-single-steps definition."""
+    _deep_halo_case(h3d, gpu, kernel, dtype, n0, box_x, side, ny)
 
 
 def _deep_halo_case(h3d, gpu, kernel, dtype, n0, box_x, side, ny=37):
     ops = h3d.ops
     head = kernel.split(":")[0]
-    K = 2 if head in ("tb2", "tbk2") else int(head[2])
+    K = int(head[2])
     n = (n0, ny, 133)
     ux = (-(K - 1) if side in ("lo", "both") else 0, n0 + (K - 1 if side in ("hi", "both") else 0))
     box = (box_x[0], box_x[1], 0, n[1], 0, n[2])
@@ -311,11 +248,11 @@ def test_temporal_mixed_steps_gpu(h3d, gpu, K, vr):
     assert np.array_equal(a.gather(), b.gather())
 
 
-@pytest.mark.parametrize("kernel2", ["tr3", "tr3:1:4:1:8:0:3", "tr2", "tr4", "tl3", "tl4", "tl2"])
+@pytest.mark.parametrize("kernel2", ["tl3", "tl4", "tl2", "tl5", "tl3:1:3:1:16:0:4", "tl4:1:6:1:8:0:3"])
 @pytest.mark.parametrize("vr", [1, 3])
-def test_ring_kernel_solver_gpu(h3d, gpu, kernel2, vr):
-    """Register-ring sweeps (stencil_tbr.hip) in the solver, single domain and
-    x slabs: bitwise equal to the CPU single-step solver, same convergence."""
+def test_lean_kernel_solver_gpu(h3d, gpu, kernel2, vr):
+    """Lean sweeps (stencil_tbl.hip) in the solver, single domain and x slabs:
+    bitwise equal to the CPU single-step solver, same convergence."""
     n = (67, 45, 131)
     a = h3d.HeatSolver(n, 10 ** 6, 1e-4, backend="hip", virtual_ranks=vr, decomp=(vr, 1, 1),
                        extra_args=["--kernel2", kernel2])
@@ -342,10 +279,10 @@ def test_pair_kernel_solver_gpu(h3d, gpu, kernel2, dtype, vr):
     assert np.array_equal(a.gather(), b.gather())
 
 
-@pytest.mark.parametrize("kernel2", ["tr3", "tr2", "tb3", "tb2", "tl3", "tl4"])
+@pytest.mark.parametrize("kernel2", ["tl2", "tl3", "tl4", "tl5"])
 def test_sweep_nan_faults(h3d, gpu, kernel2):
     """A NaN anywhere in the field reaches the convergence check as a fault
-    (the ring kernel detects it on the stored T^{n+K} and poisons every slot)."""
+    (the kernel detects it on the stored T^{n+K} and poisons every slot)."""
     s = h3d.HeatSolver((41, 37, 45), 10 ** 6, 1e-5, backend="hip", extra_args=["--kernel2", kernel2])
     s.initialize()
     s.step(12)
@@ -356,13 +293,12 @@ def test_sweep_nan_faults(h3d, gpu, kernel2):
 
 
 @pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2), (2, 1, 3), (1, 3, 1), (1, 1, 2)])
-@pytest.mark.parametrize("kernel2,dtype", [("tr3", "fp64"), ("tr2", "fp64"), ("tr4", "fp64"),
-                                           ("tr3:1:6:1:8:0:3", "fp64"), ("tr3", "fp32"), ("tr4:1:4:1:8:0:3", "fp32"),
-                                           ("tl3", "fp64"), ("tl4", "fp64"), ("tl4", "fp32"),
+@pytest.mark.parametrize("kernel2,dtype", [("tl2", "fp64"), ("tl3", "fp64"), ("tl4", "fp64"), ("tl4", "fp32"),
+                                           ("tl3:1:6:1:8:0:3", "fp64"),
                                            ("tl3:2:3:1:16:0:3", "fp32"), ("tl4:2:2:1:16:0:3", "fp32")])
-def test_block_decomposition_ring_kernel_gpu(h3d, gpu, dims, kernel2, dtype):
+def test_block_decomposition_lean_kernel_gpu(h3d, gpu, dims, kernel2, dtype):
     """Deep y / z halos (axis-ordered exchange with edges and corners) and the
-    ring kernel's y / z update ranges: virtual-rank block decompositions on
+    lean kernel's y / z update ranges: virtual-rank block decompositions on
     the GPU equal the single-domain single-step run bit for bit."""
     n = (45, 61, 150)
     P = dims[0] * dims[1] * dims[2]
@@ -377,7 +313,7 @@ def test_block_decomposition_ring_kernel_gpu(h3d, gpu, dims, kernel2, dtype):
 
 
 @pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2)])
-def test_block_decomposition_ring_kernel_rollback_gpu(h3d, gpu, dims):
+def test_block_decomposition_rollback_gpu(h3d, gpu, dims):
     P = dims[0] * dims[1] * dims[2]
     for eps in (1e-3, 9e-4, 8e-4):
         a = h3d.HeatSolver((33, 33, 33), 10 ** 6, eps, backend="hip", virtual_ranks=P, decomp=dims,
@@ -396,15 +332,14 @@ def _deep3_random(ops, n, g, dtype, seed):
     return f
 
 
-@pytest.mark.parametrize("kernel", ["tr2", "tr3", "tr4", "tr3:1:6:1:8:0:3", "tr3:1:3:1:16:0:3:1",
-                                    "tl2", "tl3", "tl4", "tl3:1:3:1:16:0:4"])
+@pytest.mark.parametrize("kernel", ["tl2", "tl3", "tl4", "tl3:1:3:1:16:0:4"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("box,sides", [((0, 12, 0, 50, 0, 140), "lo"), ((0, 12, 0, 50, 0, 140), "hi"),
                                        ((0, 12, 0, 50, 0, 140), "both"), ((0, 12, 4, 46, 0, 140), "both"),
                                        ((3, 9, 0, 4, 0, 140), "both"), ((0, 12, 46, 50, 5, 135), "both"),
                                        ((0, 12, 0, 50, 136, 140), "both"), ((2, 10, 3, 47, 0, 4), "both")])
 def test_sweep_deep_yz_halo_matches_cpu(h3d, gpu, kernel, dtype, box, sides):
-    """Deep ghosts on every axis (block decompositions): the ring kernel's
+    """Deep ghosts on every axis (block decompositions): the lean kernel's
     y / z update ranges and its residual (only the box widened by K-1-s
     counts at stage s) equal the CPU K-single-steps definition on random
     fields, for thin / partial boxes such as the interior/boundary pieces."""
@@ -455,15 +390,14 @@ def _deep_yz_case(h3d, gpu, kernel, dtype, box, sides):
 
 @pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2), (2, 1, 3)])
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
-def test_block_overlap_gpu(h3d, gpu, dims, dtype, monkeypatch):
+def test_block_overlap_gpu(h3d, gpu, dims, dtype):
     """Overlapped block sweeps on the GPU (three streams, lagged check) equal
     the exchange-first schedule and the single-domain run bit for bit."""
     P = dims[0] * dims[1] * dims[2]
     n = (61, 67, 150)
     a = h3d.HeatSolver(n, 31, 0.0, dtype=dtype, backend="hip", virtual_ranks=P, decomp=dims)
-    monkeypatch.setenv("HEAT3D_BLOCK_OVERLAP", "0")
-    b = h3d.HeatSolver(n, 31, 0.0, dtype=dtype, backend="hip", virtual_ranks=P, decomp=dims)
-    monkeypatch.delenv("HEAT3D_BLOCK_OVERLAP")
+    b = h3d.HeatSolver(n, 31, 0.0, dtype=dtype, backend="hip", virtual_ranks=P, decomp=dims,
+                       extra_args=["--no-block-overlap"])
     c = h3d.HeatSolver(n, 31, 0.0, dtype=dtype, backend="hip")
     assert a.native.field_buffers == 3 and b.native.field_buffers == 2
     ra, rb, rc = a.run(), b.run(), c.run()
@@ -481,4 +415,19 @@ def test_aligned_z_stride_solver_gpu(h3d, gpu):
     b = h3d.HeatSolver(n, 31, 0.0, backend="cpu", extra_args=["--temporal", "1"])
     ra, rb = a.run(), b.run()
     assert ra["iterations"] == rb["iterations"] == 31 and ra["last_residual"] == rb["last_residual"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("iters", [7, 11, 12])
+def test_temporal_k5_remainders(h3d, gpu, dtype, iters):
+    """--temporal 5 with step counts that are not multiples of 5: the K+1 = 6
+    long sweeps are taken only where that variant exists (fp32; fp64 has no
+    K = 6 shape and falls back to partial sweeps) — bitwise equal to single
+    steps either way (a K = 6 sweep used to be issued and throw)."""
+    a = h3d.HeatSolver((41, 37, 45), iters, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "5"])
+    b = h3d.HeatSolver((41, 37, 45), iters, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
+    assert a.native.temporal_steps == 5
+    ra, rb = a.run(), b.run()
+    assert ra["iterations"] == rb["iterations"] == iters and ra["last_residual"] == rb["last_residual"]
     assert np.array_equal(a.gather(), b.gather())

@@ -160,13 +160,12 @@ def test_phase_timers(h3d):
 
 @pytest.mark.parametrize("rank,size,decomp,temporal", [(1, 4, (4, 1, 1), "3"), (0, 2, (2, 1, 1), "1"),
                                                        (3, 8, (2, 2, 2), "3")])
-def test_phantom_rank_proxy_runs(h3d, rank, size, decomp, temporal, monkeypatch):
+def test_phantom_rank_proxy_runs(h3d, rank, size, decomp, temporal):
     """PhantomComm (tools/rank_proxy.py): one rank of a P-rank job alone in the
     process builds only its subdomain and runs its whole schedule, every
     issued iteration accounted for, nothing converges at eps 0."""
-    monkeypatch.setenv("HEAT3D_PHANTOM_ALLREDUCE_US", "0")
     s = h3d.HeatSolver((20, 20, 20), 1 << 40, 0.0, backend="cpu", decomp=decomp, phantom=(rank, size),
-                       threads=2, extra_args=["--temporal", temporal])
+                       threads=2, extra_args=["--temporal", temporal, "--phantom-allreduce-us", "0"])
     assert s.native.comm_name == "phantom"
     s.initialize()
     s.step(13)
@@ -211,7 +210,7 @@ def test_checkpoint_crash_safety_and_checksum(h3d, tmp_path):
         h3d.HeatSolver((19, 17, 21), 60, 0.0, backend="cpu", extra_args=["--restart", str(ck)]).run()
 
 
-def test_streamed_io_bounded_chunks(h3d, tmp_path, monkeypatch):
+def test_streamed_io_bounded_chunks(h3d, tmp_path):
     """With a 1 MiB staging chunk the checkpoint, the per-rank Tecplot zones
     and the root gather stream in many chunks and give the same bytes."""
     import filecmp
@@ -221,8 +220,8 @@ def test_streamed_io_bounded_chunks(h3d, tmp_path, monkeypatch):
     s.write_tecplot(str(tmp_path / "a.dat"), "owned")
     s.save_checkpoint(str(tmp_path / "ca"))
     g = s.gather()
-    monkeypatch.setenv("HEAT3D_IO_STAGE_MB", "1")
-    t = h3d.HeatSolver((37, 29, 33), 30, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1))
+    t = h3d.HeatSolver((37, 29, 33), 30, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1),
+                       extra_args=["--io-stage-mb", "1"])
     t.run()
     t.write_tecplot(str(tmp_path / "b.dat"), "owned")
     t.save_checkpoint(str(tmp_path / "cb"))
@@ -233,15 +232,14 @@ def test_streamed_io_bounded_chunks(h3d, tmp_path, monkeypatch):
     assert len(zones) == 4 and sum(np.prod(z["shape"]) for z in zones) == 37 * 29 * 33
 
 
-def test_gather_refuses_oversized_grid(h3d, monkeypatch):
-    s = h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu")
+def test_gather_refuses_oversized_grid(h3d):
+    s = h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu", extra_args=["--host-mem-limit-gb", "0.0001"])
     s.run()
-    monkeypatch.setenv("HEAT3D_HOST_MEM_LIMIT_GB", "0.0001")
     with pytest.raises(Exception, match="host memory"):
         s.gather()
 
 
-def test_memory_preflight(h3d, monkeypatch):
+def test_memory_preflight(h3d):
     """Buffers are sized before any allocation: a configuration that does not
     fit the backend's free memory is refused with the numbers (here host RAM;
     HBM via hipMemGetInfo on the GPU backend, tests/test_gpu_solver.py)."""
@@ -256,8 +254,7 @@ def test_memory_preflight(h3d, monkeypatch):
     assert p.native.planned_bytes > p.native.field_buffers * 24 ** 3 * 8
     with pytest.raises(Exception, match="memory preflight.*needs"):
         h3d.HeatSolver((6000, 6000, 6000), 5, 0.0, backend="cpu")
-    monkeypatch.setenv("HEAT3D_MEM_RESERVE_GB", str(n.mem_free_before / 1e9))
+    reserve = ["--mem-reserve-gb", str(n.mem_free_before / 1e9)]
     with pytest.raises(Exception, match="memory preflight"):
-        h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu")
-    monkeypatch.setenv("HEAT3D_MEM_PREFLIGHT", "0")
-    h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu")
+        h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu", extra_args=reserve)
+    h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu", extra_args=reserve + ["--no-mem-preflight"])

@@ -3,7 +3,7 @@ backend: the sweep schedule (interior planes || deep halo -> boundary slabs,
 convergence rollback) must reproduce the single-step solver bit for bit for
 every depth K, slab count, overlap mode and iteration count.  The CPU
 backend's multi-step sweep is the K-single-steps definition of the gfx950
-kernels (stencil_tb2.hip, stencil_tbk.hip)."""
+kernel (stencil_tbl.hip / stencil_tbp.hip)."""
 import numpy as np
 import pytest
 
@@ -80,14 +80,15 @@ def test_single_plane_slabs_fall_back(h3d):
 
 
 def test_block_decomposition_uses_lean_kernel(h3d):
-    # y / z splits take temporal blocking too, with a kernel that has y / z
-    # update ranges: the lean kernel by default, the ring kernel on request
+    # y / z splits take temporal blocking too, with the lean kernel's y / z
+    # update ranges; the retired round-1/2 kernel families are refused
     s = h3d.HeatSolver((17, 17, 17), 10, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1), extra_args=T2)
     assert s.native.temporal_blocking and s.native.temporal_steps == 2
     assert s.native.kernel_name.startswith("tl2"), s.native.kernel_name
-    s = h3d.HeatSolver((17, 17, 17), 10, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1),
-                       extra_args=T2 + ["--kernel2", "tr2"])
-    assert s.native.kernel_name.startswith("tr2"), s.native.kernel_name
+    for old in ("tr2", "tb2", "tbk2", "tb3"):
+        with pytest.raises(Exception, match="retired"):
+            h3d.HeatSolver((17, 17, 17), 10, 0.0, backend="cpu", virtual_ranks=4, decomp=(2, 2, 1),
+                           extra_args=T2 + ["--kernel2", old])
 
 
 def test_slab_pairs_verify_halos(h3d):
@@ -125,7 +126,7 @@ def test_cpu_sweep_definition(h3d, K, box_x, ux):
     f.deep().copy_(torch.rand(f.deep().shape, generator=g, dtype=torch.float64))
     out = ops.PaddedField(n, gx=K)
     ops.sweep(f, out, (0.07, 0.05, 0.03), (box_x[0], box_x[1], 0, n[1], 0, n[2]), ux,
-              kernel="tb2" if K == 2 else f"tb{K}")
+              kernel=f"tl{K}")
     T = f.deep().clone()  # plane index i <-> T[i + K]
     for s in range(K):
         w = K - 1 - s
@@ -137,18 +138,16 @@ def test_cpu_sweep_definition(h3d, K, box_x, ux):
 
 
 @pytest.mark.parametrize("K", [2, 3, 4])
-def test_lagged_check_uses_three_buffers(h3d, K, monkeypatch):
+def test_lagged_check_uses_three_buffers(h3d, K):
     """Overlapped x-slab sweeps lag the convergence check by one sweep (third
-    field buffer, two residual-slot banks); HEAT3D_LAG=0 restores the
+    field buffer, two residual-slot banks); --lag off restores the
     ping-pong schedule.  Both converge at the same iteration to the same field,
     with the converged iteration landing at every offset inside a sweep."""
     for eps in (1e-3, 9e-4, 8e-4, 7e-4):
         a, b = _pair(h3d, (37, 21, 19), 10 ** 6, eps, 3, K=K, extra=["--check-every", "5"])
         assert a.native.field_buffers == 3
-        monkeypatch.setenv("HEAT3D_LAG", "0")
         c = h3d.HeatSolver((37, 21, 19), 10 ** 6, eps, backend="cpu", virtual_ranks=3, decomp=(3, 1, 1),
-                           extra_args=["--temporal", str(K), "--check-every", "5"])
-        monkeypatch.delenv("HEAT3D_LAG")
+                           extra_args=["--temporal", str(K), "--check-every", "5", "--lag", "off"])
         assert c.native.field_buffers == 2 and b.native.field_buffers == 2
         ra, rb, rc = a.run(), b.run(), c.run()
         assert ra["conv_iter"] == rb["conv_iter"] == rc["conv_iter"] and ra["converged"]
@@ -224,19 +223,17 @@ def test_partial_sweep_remainders(h3d, K, vr, dims, iters):
 
 
 @pytest.mark.parametrize("dims", [(2, 2, 2), (1, 2, 2), (2, 1, 3)])
-def test_block_overlap_matches_exchange_first(h3d, dims, monkeypatch):
+def test_block_overlap_matches_exchange_first(h3d, dims):
     """Overlapped block sweeps (interior || axis-ordered halo -> onion of
     boundary pieces, lagged check on three buffers) equal the exchange-first
-    schedule (HEAT3D_BLOCK_OVERLAP=0) bit for bit, converged or not."""
+    schedule (--no-block-overlap) bit for bit, converged or not."""
     P = dims[0] * dims[1] * dims[2]
     n = (31, 29, 33)
     for eps in (0.0, 8e-4):
         a = h3d.HeatSolver(n, 10 ** 6 if eps else 25, eps, backend="cpu", virtual_ranks=P, decomp=dims,
                            extra_args=["--temporal", "3", "--check-every", "5"])
-        monkeypatch.setenv("HEAT3D_BLOCK_OVERLAP", "0")
         b = h3d.HeatSolver(n, 10 ** 6 if eps else 25, eps, backend="cpu", virtual_ranks=P, decomp=dims,
-                           extra_args=["--temporal", "3", "--check-every", "5"])
-        monkeypatch.delenv("HEAT3D_BLOCK_OVERLAP")
+                           extra_args=["--temporal", "3", "--check-every", "5", "--no-block-overlap"])
         assert a.native.field_buffers == 3 and b.native.field_buffers == 2
         ra, rb = a.run(), b.run()
         assert ra["conv_iter"] == rb["conv_iter"] and ra["last_residual"] == rb["last_residual"]

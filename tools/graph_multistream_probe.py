@@ -29,8 +29,6 @@ def main() -> int:
     ap.add_argument("--phantom", default="", help="R/P: run rank R of a P-rank job (PhantomComm)")
     args = ap.parse_args()
 
-    # multi-stream schedules are graphs only on request (solver.cpp graphs_allowed)
-    os.environ.setdefault("HEAT3D_GRAPH_MULTISTREAM", "1")
     import numpy as np
 
     import heat3d_amd
@@ -40,7 +38,9 @@ def main() -> int:
     N = (args.n,) * 3
 
     def solve(graph: bool):
-        kw = dict(dtype=args.dtype, backend="hip", decomp=dims, graph=graph, graph_chunk=36, device=0)
+        # multi-stream schedules are graphs only on request (solver.cpp graphs_allowed)
+        kw = dict(dtype=args.dtype, backend="hip", decomp=dims, graph=graph, graph_chunk=36, device=0,
+                  extra_args=["--graph-multistream"])
         if args.phantom:
             r, p = (int(v) for v in args.phantom.split("/"))
             s = HeatSolver(N, iter_max=1 << 30, eps=0.0, phantom=(r, p), **kw)

@@ -39,8 +39,6 @@ def main() -> int:
     ap.add_argument("--extra", default="", help="extra solver flags, e.g. '--no-overlap'")
     args = ap.parse_args()
 
-    os.environ["HEAT3D_PHANTOM_GBPS"] = str(args.gbps)
-    os.environ["HEAT3D_PHANTOM_ALLREDUCE_US"] = str(args.ar_us)
     from heat3d_amd import HeatSolver
     from heat3d_amd.parallel import best_dims_for
 
@@ -54,7 +52,8 @@ def main() -> int:
     gb = lambda b: None if b is None else round(b / 1e9, 2)
     s = HeatSolver(N, iter_max=1 << 40, eps=0.0, dtype=args.dtype, backend=args.backend, decomp=dims,
                    device=0 if args.backend == "hip" else None, phantom=(r, P),
-                   extra_args=args.extra.split() if args.extra else ())
+                   extra_args=["--phantom-gbps", str(args.gbps), "--phantom-allreduce-us", str(args.ar_us)]
+                   + (args.extra.split() if args.extra else []))
     s.initialize()
     free_after, total = s.native.mem_info()
     s.step(args.warmup)

@@ -5,7 +5,7 @@ Times ``ftcs_step`` ping-pong sweeps over an N^3 box for each kernel variant,
 alternating variants round by round (cdna_hip_programming.md §5.4 rule 24),
 and prints GLUPS / effective TB/s (16 B/point fp64, 8 B/point fp32).
 
-  python tools/tune.py --n 1024 --dtype fp64 --variants column:2:8 column:1:4 naive
+  python tools/tune.py --n 1024 --dtype fp64 --variants tl3 tl4 tile naive
 """
 import argparse
 import json
@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--dtype", default="fp64")
-    ap.add_argument("--variants", nargs="+", default=["column"])
+    ap.add_argument("--variants", nargs="+", default=["tl3"])
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json-out", default="")
@@ -52,7 +52,7 @@ def main():
     res = {v: [] for v in a.variants}
     def steps(v):  # time steps per sweep of a variant
         head = v.split(":")[0]
-        return 2 if head in ("tb2", "tbk2") else int(head[2]) if head[:2] in ("tb", "tr", "tl") else 1
+        return int(head[2]) if head[:2] == "tl" else 1
 
     def run(v, a_, b_):
         (ops.ftcs_step2 if steps(v) > 1 else ops.ftcs_step)(a_, b_, D, kernel=v, state=state)
