@@ -199,8 +199,9 @@ int main(int argc, char** argv) {
   try {
     cfg = Config::parse(argc, argv);
   } catch (const UsageError& e) {
-    const char* r = std::getenv("RANK");
-    if (!r || std::atoi(r) == 0) {
+    // every rank validates (reference heat3D.cu:284-292 checked on rank 0
+    // only and let the others run on into stoi); rank 0 prints
+    if (rank_from_env() == 0) {
       std::cout << Config::usage() << std::flush;
       std::cerr << "heat3d: " << e.what() << std::endl;
     }

@@ -75,7 +75,7 @@ struct Config {
   bool block_overlap = true;      // block decompositions: interior || halo (false: exchange first)
   bool long_sweeps = true;        // K+1-step sweeps absorb step counts that are not multiples of K
   bool graph_multistream = false; // record the overlapped multi-stream schedule into hipGraphs too
-  bool rccl_graph = false;        // RCCL calls may be recorded into hipGraphs (single-stream schedules)
+  bool rccl_graph = true;         // RCCL calls may be recorded into hipGraphs (tests/test_gpu_rccl.py)
   bool rccl_shared = false;       // one RCCL communicator for halos and all-reduces (else ncclCommSplit)
   double mem_reserve_gb = 2.0;    // memory preflight: reserve for RCCL, code objects, scratch
   bool mem_preflight = true;      // refuse configurations that do not fit before allocating

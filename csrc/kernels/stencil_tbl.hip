@@ -363,6 +363,7 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
 template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
 static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   constexpr bool swap_xy = SW;
+  const void* kfn = reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW>);
   Box b = p.box;
   constexpr int TY = WY * R;
   // swap_xy: march along y with x as the tile rows (thin x slabs: a tile of
@@ -411,8 +412,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live + 1 && g.ulo <= b.lo[0] && g.uhi >= b.hi[0],
                "tl: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
   constexpr int YS = TY - 2 * K;
-  static const int slots =  // magic static: thread-safe under --gpus N
-      device_slots(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW>), 64 * WY);
+  static const int slots = device_slots(kfn, 64 * WY);  // magic static: thread-safe under --gpus N
   constexpr int U = Q == 4 ? 12 : 6;  // the kernel's unroll (lcm(Q, 3, 2))
   const int ZS = lean_z_stride(b.extent(0), b.extent(1), b.extent(2), K, (int)sizeof(Real), TY, slots, U, ks.L);
   g.zs = ZS;
@@ -433,11 +433,9 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
     std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: seg=%d tiles=%dx%d blocks=%lld\n", K, (long long)nxb,
                  xp.seg, g.nzb, g.nyb, (long long)nblocks);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl: residual slots " << p.slot << "+" << K);
-  static const int spill = [] {
+  static const int spill = [kfn] {
     hipFuncAttributes a{};
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW>)) == hipSuccess
-               ? (int)a.localSizeBytes
-               : 0;
+    return hipFuncGetAttributes(&a, kfn) == hipSuccess ? (int)a.localSizeBytes : 0;
   }();
   // a spilling variant is refused (one was miscompiled on ROCm 7.2)
   HEAT3D_CHECK(spill == 0, "tl variant " << ks.str() << " spills " << spill << " B of registers per lane");
@@ -496,8 +494,9 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
   H3D_TBL(2, 16, 4, 6) H3D_TBL(2, 16, 3, 6) H3D_TBL(3, 16, 3, 6) H3D_TBL(2, 16, 2, 6)
   H3D_TBL(3, 16, 2, 3) H3D_TBL(2, 16, 2, 3)
   H3D_TBL(4, 12, 4, 3) H3D_TBL(4, 12, 4, 4) H3D_TBL(4, 12, 5, 3) H3D_TBL(3, 12, 5, 3) H3D_TBL(3, 12, 4, 3)
-  // 8 waves (<= 256 VGPRs, 2 per SIMD): 48-row tiles at K = 4
+  // 8 waves (<= 256 VGPRs, 2 per SIMD): 48-row tiles at K = 4; the fp64 K = 5 / 6 defaults
   H3D_TBL(6, 8, 4, 3) H3D_TBL(6, 8, 3, 3) H3D_TBL(6, 8, 4, 4) H3D_TBL(5, 8, 4, 3)
+  H3D_TBL(3, 8, 5, 3) H3D_TBL(3, 8, 6, 3)
   if constexpr (sizeof(Real) == 4) {
     // fp32: half the registers and LDS per row, so deeper sweeps fit 16 waves
     H3D_TBL(4, 16, 4, 3) H3D_TBL(3, 16, 5, 3) H3D_TBL(4, 16, 5, 3) H3D_TBL(3, 16, 6, 3)
@@ -522,7 +521,7 @@ void stencil_lean(DType t, const StencilParams& p, const KernelSpec& k, void* st
 }
 
 void sweep(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
-  HEAT3D_CHECK(k.kind == KernelSpec::TBL, "sweep needs a K-step kernel (tl2..tl6)");
+  HEAT3D_CHECK(k.multi_step(), "sweep needs a K-step kernel (tl2..tl6)");
   stencil_lean(t, p, k, stream);
 }
 

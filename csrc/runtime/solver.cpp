@@ -67,7 +67,7 @@ KernelSpec KernelSpec::parse(const std::string& s) {
   } else if (h == "tile" || (h.size() == 3 && h[0] == 't' && h[1] == 'l' && h[2] >= '2' && h[2] <= '6')) {
     // tile = single step; tl2..tl6 = K-step lean sweep kernel
     k.kind = h == "tile" ? Tile : TBL;
-    if (k.kind == TBL) k.K = h[2] - '0';
+    if (k.kind != Tile) k.K = h[2] - '0';
     auto at = [&](std::size_t i) { return parts.size() > i ? std::atoi(parts[i].c_str()) : 0; };
     k.V = at(1);
     k.R = at(2);
@@ -75,7 +75,7 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     k.WY = at(4);
     k.L = at(5);
     k.NT = at(6);
-    if (k.kind == TBL && parts.size() > 7) k.O = at(7);  // store cache-policy bits
+    if (k.kind != Tile && parts.size() > 7) k.O = at(7);  // store cache-policy bits
   } else if (h == "column" || h == "tb2" || h == "tbk2" || (h.size() == 3 && h[0] == 't' && (h[1] == 'b' || h[1] == 'r'))) {
     throw UsageError("kernel '" + s + "' was retired in round 3 (the column / queue / register-ring kernels); "
                      "use tile for single steps and tl2..tl6 for K-step sweeps");
@@ -112,7 +112,13 @@ KernelSpec KernelSpec::resolved(DType t) const {
         r.R = 3;
         r.WY = 12;
       }
-      def(r.R, (f64 || r.V == 2) ? (K >= 4 ? 2 : 3) : (K >= 4 && K <= 5 ? 4 : 3));
+      // fp64 K = 5 / 6 and fp32 K = 6: no 16-wave shape fits 128 VGPRs
+      // without spilling; 8 waves of 3 rows (24-row tiles, up to 256 VGPRs)
+      if ((f64 ? K >= 5 : K >= 6) && r.V == 1 && r.R == 0 && r.WY == 0) {
+        r.R = 3;
+        r.WY = 8;
+      }
+      def(r.R, (f64 || r.V == 2) ? (K >= 4 ? 2 : 3) : (K == 4 ? 4 : 3));
       def(r.WZ, 1);
       def(r.WY, 16);
       def(r.NT, 3);
@@ -142,7 +148,7 @@ std::string KernelSpec::str() const {
   std::ostringstream os;
   os << (kind == Tile ? std::string("tile:") : "tl" + std::to_string(K) + ":") << V << ":" << R << ":" << WZ << ":"
      << WY << ":" << L << ":" << NT;
-  if (kind == TBL && O > 0) os << ":" << O;
+  if (kind != Tile && O > 0) os << ":" << O;
   return os.str();
 }
 
@@ -179,8 +185,8 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
           : dt_ == DType::F64    ? kDefaultTemporal
                                  : kDefaultTemporalF32;
   // the sweep kernel: the lean kernel (stencil_tbl.hip; fp32 its packed-pair
-  // form, stencil_tbp.hip); --kernel2 tlK:... picks a variant
-  kspec2_.kind = KernelSpec::TBL;
+  // form, stencil_tbp.hip); --kernel2 tlK:... / tsK:... picks a variant
+  if (!kspec2_.multi_step()) kspec2_.kind = KernelSpec::TBL;
   kspec2_.K = K;
   int64_t min_n[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
   for (const auto& sd : dec_.subs)
@@ -640,7 +646,7 @@ void Solver::enqueue_multi(int bi, int Kp) {
     // partial (Kp < K) or long (Kp = K + 1, single subdomain) sweep: the
     // kernel family's default variant of depth Kp
     ks = KernelSpec();
-    ks.kind = KernelSpec::TBL;
+    ks.kind = kspec2_.kind;
     ks.K = Kp;
   }
   // update ranges reach Kp - 1 (not K_ - 1) points into the deep halos
@@ -931,14 +937,14 @@ int Solver::graph_len_for(int64_t n) const {
 }
 
 int Solver::long_sweeps_for(int64_t n) const {
-  if (!tb_ || has_halo_ || kspec2_.kind != KernelSpec::TBL || n % K_ == 0) return 0;
+  if (!tb_ || has_halo_ || !kspec2_.multi_step() || n % K_ == 0) return 0;
   if (K_ + 1 > 6 || K_ + 1 > kResidualSlots) return 0;
   const int64_t b = n % K_;             // n = a K + b (K + 1) with a = (n - b (K + 1)) / K
   if (b * (K_ + 1) > n) return 0;
   if (!cfg_.long_sweeps) return 0;
   // the K+1 variant must exist for this dtype (e.g. fp64 K = 5 has no K = 6)
   KernelSpec ks;
-  ks.kind = KernelSpec::TBL;
+  ks.kind = kspec2_.kind;
   ks.K = K_ + 1;
   return be_->is_gpu() && !hip::lean_supported(dt_, ks) ? 0 : (int)b;
 }
@@ -1818,9 +1824,11 @@ static int env_int(const char* a, const char* b, int dflt) {
   return (v && *v) ? std::atoi(v) : dflt;
 }
 
+int rank_from_env() { return env_int("RANK", "OMPI_COMM_WORLD_RANK", env_int("PMI_RANK", nullptr, 0)); }
+
 std::unique_ptr<Solver> make_solver_from_env(const Config& cfg) {
   RankPlacement w;
-  w.rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", env_int("PMI_RANK", nullptr, 0));
+  w.rank = rank_from_env();
   w.size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", env_int("PMI_SIZE", nullptr, 1));
   w.local_rank = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", env_int("MPI_LOCALRANKID", nullptr, w.rank));
   const char* ma = std::getenv("MASTER_ADDR");

@@ -349,5 +349,8 @@ std::unique_ptr<Solver> make_solver(const Config& cfg, const RankPlacement& wher
 // Same, placement from the environment: RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT (torchrun / mpirun style).
 std::unique_ptr<Solver> make_solver_from_env(const Config& cfg);
+// This process's rank as the launcher tells it: RANK (torchrun),
+// OMPI_COMM_WORLD_RANK (Open MPI) or PMI_RANK (MPICH hydra); 0 without one.
+int rank_from_env();
 
 }  // namespace heat3d

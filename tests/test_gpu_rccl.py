@@ -87,15 +87,17 @@ def test_bench_self_launch_socket(gpu, tmp_path):
     assert j["metric"].endswith("128^3 fp64 grid") and j["config"]["model"].endswith("128^3 fp64 grid")
 
 
-@pytest.mark.parametrize("world,decomp", [(2, (2, 1, 1)), (4, (2, 2, 1))])
-def test_rccl_graph_bitwise(h3d, gpu, tmp_path, world, decomp):
+@pytest.mark.parametrize("world,decomp,schedule", [(2, (2, 1, 1), ["--no-overlap"]), (4, (2, 2, 1), ["--no-overlap"]),
+                                                   (2, (2, 1, 1), ["--graph-multistream"])])
+def test_rccl_graph_bitwise(h3d, gpu, tmp_path, world, decomp, schedule):
     """RCCL send / recv groups and all-reduces recorded into hipGraphs
-    (--rccl-graph, single-stream schedule): the ranks replay graphs
-    (graph_launches > 0), exit cleanly and give the field of the eager
-    single-process solve bit for bit.  Reference per-iteration comm:
-    heat3D.cu:619-641 (halo), 1062-1063 (reduction)."""
+    (--rccl-graph, the default): the single-stream schedule, and the
+    overlapped three-stream schedule with --graph-multistream.  The ranks
+    replay graphs (graph_launches > 0), exit cleanly and give the field of
+    the eager single-process solve bit for bit.  Reference per-iteration
+    comm: heat3D.cu:619-641 (halo), 1062-1063 (reduction)."""
     n, eps = 33, 1e-4
-    extra = ["--no-overlap", "--rccl-graph", "--watchdog", "60"]
+    extra = schedule + ["--rccl-graph", "--watchdog", "60"]
     mp.start_processes(native_rccl_gpu_worker,
                        args=(world, free_port(), str(tmp_path), n, eps, decomp, "fp64", extra),
                        nprocs=world, join=True, start_method="spawn")

@@ -1,0 +1,63 @@
+"""The reference's launch contract under a real MPI launcher.
+
+``mpirun -n P ./heat3D NX NY NZ ITER_MAX EPS`` (heat3D.cu:203-205 MPI_Init /
+rank / size, 270-315 argument check and echo, 1078-1106 report).  MPICH's
+hydra launcher (``mpirun``, present in this image) starts P processes of the
+native CLI; each takes its rank from PMI_RANK / PMI_SIZE
+(``make_solver_from_env``, csrc/runtime/solver.cpp), the ranks meet through
+the TCP bootstrap and exchange halos over the socket transport (CPU backend:
+no GPU here).  Rank 0 alone prints the banner and the report, the converged
+iteration is the single-domain golden (decomposition-independent results),
+and a wrong argument count prints the usage once and fails every rank.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import free_port
+
+MPIRUN = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+pytestmark = pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun in this image")
+
+_LAUNCHER_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                  "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "PMI_RANK", "PMI_SIZE")
+
+
+def _mpirun(heat3d_bin, n, args, cwd, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_VARS}
+    env["HEAT3D_BOOTSTRAP_PORT"] = str(free_port())
+    return subprocess.run([MPIRUN, "-n", str(n), heat3d_bin] + list(args), cwd=cwd, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n,decomp", [(4, None), (2, "1x2x1")])
+def test_mpirun_reference_launch(heat3d_bin, tmp_path, n, decomp):
+    args = ["33", "33", "33", "100000", "1e-5", "--backend", "cpu", "--comm", "socket", "--threads", "2"]
+    if decomp:
+        args += ["--decomp", decomp]
+    r = _mpirun(heat3d_bin, n, args, tmp_path)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = r.stdout
+    # one banner and one report for the whole job (rank 0), not one per process
+    assert out.count("Runnung HeatEquation3D with the following arguments:") == 1, out
+    assert out.count("Computational time (parallel): ") == 1
+    assert out.count("L2-norm error:") == 1
+    assert f"comm=socket ranks={n}" in out
+    # App. B.3 golden of the single domain: the decomposition changes nothing
+    assert "Simulation has converged in 3590 iterations with a convergence threshold of 1.000000e-05" in out
+    assert "L2-norm error: 0.0287 %" in out
+    # output/out.dat written once, one zone per rank with the rank column (heat3D.cu:1125-1162)
+    lines = (tmp_path / "output" / "out.dat").read_text().split("\n")
+    assert lines[0] == 'TITLE="out"' and lines[1] == 'VARIABLES = "X", "Y", "Z", "T", "rank"'
+    assert sum(1 for l in lines if l.startswith("ZONE T = ")) == n
+
+
+def test_mpirun_usage_error(heat3d_bin, tmp_path):
+    """A wrong argument count: the usage text once (rank 0), every rank exits
+    non-zero (the reference let ranks > 0 run on into stoi)."""
+    r = _mpirun(heat3d_bin, 3, ["33", "33"], tmp_path, timeout=60)
+    assert r.returncode != 0
+    assert r.stdout.count("Incorrect number of command line arguments specified") == 1, r.stdout
+    assert not (tmp_path / "output").exists()

@@ -55,7 +55,7 @@ rccl_ranks() {  # $1 = n, $2 = tag, $3 = 1 to trace, rest = bench args
 
 for step in "$@"; do
   i=$((i + 1))
-  read -r -a a <<< "$step"
+  eval "a=($step)"  # quotes inside a step group words, e.g. 'suite tests/ -k "a or b"' 
   name=${a[0]}
   args=("${a[@]:1}")
   echo "== step $i: $step"
