@@ -55,6 +55,9 @@ struct StencilParams {
   int64_t ux[2] = {0, -1};
   // same for y and z (block decompositions with deep y / z halos)
   int64_t uy[2] = {0, -1}, uz[2] = {0, -1};
+  // CUs the launch stream's CU mask keeps free (persistent sweeps launch as
+  // many workgroups as the remaining CUs hold)
+  int cu_reserved = 0;
 };
 
 struct InitParams {
@@ -86,6 +89,8 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
 // fp32 lean kernel on packed pairs of z columns (stencil_tbp.hip; spec tlK:2:…)
 void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream);
 bool lean_pair_supported(const KernelSpec& k);
+// z tile stride of the pair kernel for a box (host-side choice, stencil_tbp.hip)
+int pair_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L);
 // Is the lean kernel variant that k resolves to for dtype t instantiated?
 bool lean_supported(DType t, const KernelSpec& k);
 // Any multi-step kind -> its kernel

@@ -126,29 +126,54 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     return c * (n >> 3) + min(c, n & 7) + (i >> 3);
   };
   const int blk = blockIdx.x;
-  int pc, part;
-  const int rr = g.rb & 0x3fffffff;
-  if (blk < g.n1) {
-    pc = remap(blk, g.n1);
-    part = 0;
-  } else if (blk < g.n1 + rr) {
-    pc = g.n1 + remap(blk - g.n1, rr);
-    part = 1;
-  } else {
-    pc = g.n1 + remap(blk - g.n1 - rr, rr);
-    part = 2;
-  }
-  // tile order inside an x segment: z fastest
   const int zs = g.zs;
   const int ntile = g.nzb * g.nyb;
-  const int xs = pc / ntile;
-  const int tt = pc - xs * ntile;
-  const int zb = tt % g.nzb, ybk = tt / g.nzb;
   const int nxb = g.bhi[0] - g.blo[0];
-  const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
-  int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
-  if (part == 1 && (g.rb >> 30)) xhi_p = min(xhi_p, xlo_p + split);
-  if (part == 2) xlo_p = min(xlo_p + split, xhi_p);
+  // This workgroup's work: plane steps [w, wend) of the tile-major list
+  // (tile t, plane x) -> t * nxb + x, walked piece by piece (a piece = one
+  // tile's contiguous planes; each pays the 2(K-1)-plane pipeline fill).
+  //   * x plan (rb >= 0): one piece per block, x segments of `seg` planes
+  //     (plan_x: whole rounds of pieces, then a split tail);
+  //   * persistent (rb < 0): exactly as many blocks as the device holds at
+  //     once, each a contiguous 1/n1 of the list, so no round of workgroups
+  //     is left partly empty and a block only pays a fill where its range
+  //     crosses into the next tile.
+  int64_t w, wend;
+  if (g.rb < 0) {
+    const int64_t W = (int64_t)ntile * nxb;
+    const int e = remap(blk, g.n1);
+    w = (int64_t)e * W / g.n1;
+    wend = (int64_t)(e + 1) * W / g.n1;
+  } else {
+    int pc, part;
+    const int rr = g.rb & 0x3fffffff;
+    if (blk < g.n1) {
+      pc = remap(blk, g.n1);
+      part = 0;
+    } else if (blk < g.n1 + rr) {
+      pc = g.n1 + remap(blk - g.n1, rr);
+      part = 1;
+    } else {
+      pc = g.n1 + remap(blk - g.n1 - rr, rr);
+      part = 2;
+    }
+    const int xs = pc / ntile;
+    const int tt = pc - xs * ntile;
+    const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
+    int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
+    if (part == 1 && (g.rb >> 30)) xhi_p = min(xhi_p, xlo_p + split);
+    if (part == 2) xlo_p = min(xlo_p + split, xhi_p);
+    w = (int64_t)tt * nxb + xlo_p;
+    wend = (int64_t)tt * nxb + xhi_p;
+  }
+
+  while (w < wend) {
+  // tile order: z fastest
+  const int tt = (int)(w / nxb);
+  const int xlo_p = (int)(w - (int64_t)tt * nxb);
+  const int xhi_p = (int)min((int64_t)nxb, xlo_p + (wend - w));
+  w += xhi_p - xlo_p;
+  const int zb = tt % g.nzb, ybk = tt / g.nzb;
 
   const int wave = sgpr(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -192,7 +217,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     ybits = ((YMask)(unsigned)sgpr((int)(ybits >> 32)) << 32) | (unsigned)sgpr((int)(unsigned)ybits);
   }
 
-  // per-lane masks (constant over the sweep)
+  // per-lane masks (constant over the piece)
   const bool zin = col >= g.uzlo && col < g.uzhi;
   const bool zst = lane >= K && lane < K + zs && col >= g.blo[2] && col < g.bhi[2];
 
@@ -318,6 +343,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     });
   }
 
+  // this piece's residuals (the lane masks depend on its tile)
   if (res) {
     double mm[K];
 #pragma unroll
@@ -333,6 +359,8 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     residual_commit_block<WY, K>(res, mm, nan_seen,
                                  *reinterpret_cast<unsigned long long(*)[WY][K]>(&s_row[0][0][0][0][0]));
   }
+  if (w < wend) __syncthreads();  // the next piece rewrites the exchange buffer
+  }  // pieces
 }
 
 // Tile stride along z.  64 - 2K stored columns per 64-lane tile, or — fp64
@@ -353,8 +381,11 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
   const int64_t nyb = std::max<int64_t>(1, (ny + TY - 2 * K - 1) / (TY - 2 * K));
   auto cost = [&](int zs) {
     const int64_t tiles = std::max<int64_t>(1, (nz + zs - 1) / zs) * nyb;
-    const XPlan p = L > 0 ? fixed_xplan(nx, tiles, L) : plan_x(nx, tiles, slots, 2 * (K - 1), U, L < 0);
-    return xplan_makespan(p, nx, tiles, slots, 2 * (K - 1), U);
+    const XPlan p = L > 0 ? fixed_xplan(nx, tiles, L) : plan_x(nx, tiles, slots, 2 * (K - 1), U, L == -1);
+    const double plan = xplan_makespan(p, nx, tiles, slots, 2 * (K - 1), U);
+    if (L != 0 && L != -2) return plan;
+    const double walk = walk_makespan(nx, tiles, slots, 2 * (K - 1), U);
+    return L == -2 ? walk : std::min(plan, walk);
   };
   constexpr double kAlignedGain = 0.92;
   return cost(aligned) * kAlignedGain < cost(wide) ? aligned : wide;
@@ -422,16 +453,35 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
   const int64_t ntiles = (int64_t)g.nzb * g.nyb;
   const int64_t nxb = b.extent(0);
-  const XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
-  HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
-  g.segsplit = xp.seg | (xp.split << 16);
-  g.n1 = xp.n1;
-  g.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
-  const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
+  // workgroups the stream can hold at once (CUs kept off it by a CU mask
+  // are not there for the persistent walk)
+  const int cus = device_cus();
+  const int live = std::max(1, (int)((int64_t)slots * std::max(1, cus - p.cu_reserved) / std::max(1, cus)));
+  // spec field L: > 0 fixed segments, -1 equal segments, -2 persistent walk,
+  // -3 the x plan, 0 the cheaper of the x plan and the walk in one makespan model
+  const XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L)
+                            : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L == -1);
+  const double plan_cost = xplan_makespan(xp, nxb, ntiles, slots, 2 * (K - 1), U);
+  const double walk_cost = walk_makespan(nxb, ntiles, live, 2 * (K - 1), U);
+  const bool walk = ks.L == -2 || (ks.L == 0 && walk_cost < 0.97 * plan_cost);
+  int64_t nblocks;
+  if (walk) {
+    g.segsplit = 0;
+    g.n1 = (int)std::min<int64_t>(live, ntiles * nxb);
+    g.rb = -1;
+    nblocks = g.n1;
+  } else {
+    HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
+    g.segsplit = xp.seg | (xp.split << 16);
+    g.n1 = xp.n1;
+    g.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
+    nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
+  }
   HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
   if (std::getenv("HEAT3D_TRACE"))
-    std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: seg=%d tiles=%dx%d blocks=%lld\n", K, (long long)nxb,
-                 xp.seg, g.nzb, g.nyb, (long long)nblocks);
+    std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: %s seg=%d tiles=%dx%d blocks=%lld (plan %.1f walk %.1f)\n",
+                 K, (long long)nxb, walk ? "walk" : "plan", xp.seg, g.nzb, g.nyb, (long long)nblocks, plan_cost,
+                 walk_cost);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl: residual slots " << p.slot << "+" << K);
   static const int spill = [kfn] {
     hipFuncAttributes a{};

@@ -173,6 +173,9 @@ PYBIND11_MODULE(_heat3d, m) {
   m.def("lean_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U) {
     return heat3d::hip::lean_z_stride(nx, ny, nz, K, esize, TY, slots, U, 0);
   });
+  m.def("pair_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U) {
+    return heat3d::hip::pair_z_stride(nx, ny, nz, K, TY, slots, U, 0);
+  });
   // a kernel spec with its per-dtype defaults filled in, as the solver
   // launches it (tests/test_temporal_cpu.py)
   m.def("kernel_spec_resolved", [](const std::string& spec, const std::string& dtype) {

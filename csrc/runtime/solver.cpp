@@ -663,6 +663,7 @@ void Solver::enqueue_multi(int bi, int Kp) {
     for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
     sp.state = dstate_;
     sp.slot = slot0;
+    sp.cu_reserved = be_->reserved_cus();
     shrink(l.ux, l.sd.n[0], sp.ux);
     shrink(l.uy, l.sd.n[1], sp.uy);
     shrink(l.uz, l.sd.n[2], sp.uz);
@@ -1525,7 +1526,10 @@ void Solver::write_tecplot_zones(const std::string& path) {
       be_->copy(host.data(), stage, ex * ey * nk * esize_, CopyKind::D2H, kCompute);
       be_->sync(kCompute);
       text.resize((std::size_t)(nk * ey * ex * line));
-#pragma omp parallel for schedule(static)
+      // no exception may leave the parallel region (std::terminate): a bad
+      // line width is flagged and thrown after it
+      int bad_width = 0;
+#pragma omp parallel for schedule(static) reduction(max : bad_width)
       for (int64_t kk = 0; kk < nk; ++kk) {
         char buf[128];  // one line: 4 x 15 + 5 + 1 characters
         const double zc = (double)(g.lo[2] + k0 + kk) * phys_.h[2];
@@ -1539,12 +1543,19 @@ void Solver::write_tecplot_zones(const std::string& path) {
                                                : (double)reinterpret_cast<const float*>(host.data())[idx];
             int w = std::snprintf(buf, sizeof(buf), "%15.5e%15.5e%15.5e%15.5e", xc, yc, zc, v);
             if (rank_column) w += std::snprintf(buf + w, sizeof(buf) - w, "%5d", r);
-            HEAT3D_CHECK(w == line - 1, "tecplot: line width " << w << " != " << line - 1);
+            if (w != line - 1) {
+              bad_width = std::max(bad_width, w + 1);
+              w = std::min(w, (int)line - 1);
+            }
             std::memcpy(o, buf, w);
             o[w] = '\n';
             o += line;
           }
         }
+      }
+      if (bad_width) {
+        io::close_raw(fd);
+        HEAT3D_THROW("tecplot: line width " << bad_width - 1 << " != " << line - 1);
       }
       io::pwrite_all(fd, text.data(), text.size(), body + k0 * ey * ex * line);
     }
@@ -1649,8 +1660,14 @@ void Solver::save_checkpoint(const std::string& dir) {
                           ", " + std::to_string(dec_.topo.dims[2]) + "]");
     j.set("layout", std::string("global z-fastest, N0*N1*N2 values"));
     io::write_file_atomic(dir + "/meta.json", j.dump() + "\n");
+    // older field files, and the temp files of saves that a crash
+    // interrupted (a full-grid field.<iter>.raw.tmp each)
+    auto ends_with = [](const std::string& s, const char* suf) {
+      const std::size_t n = std::strlen(suf);
+      return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
+    };
     for (const std::string& old : io::list_dir(dir)) {
-      const bool is_field = old.rfind("field.", 0) == 0 && old.size() > 4 && old.compare(old.size() - 4, 4, ".raw") == 0;
+      const bool is_field = old.rfind("field.", 0) == 0 && (ends_with(old, ".raw") || ends_with(old, ".raw.tmp"));
       if (is_field && old != name) io::remove_file(dir + "/" + old);
     }
   }

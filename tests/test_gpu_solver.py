@@ -57,6 +57,19 @@ def test_golden_257_slabs_gpu(h3d, gpu):
     assert r["conv_iter"] == it and abs(r["error_percent"] - err) < 6e-5, r
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("vr", [1, 8])
+def test_golden_513_gpu(h3d, gpu, vr):
+    """Round-3 golden beyond the survey's sizes: 513^3 at eps 1e-3 converges
+    at 2132 iterations, 42.7695 % (native CPU backend, 270 s on 6 threads;
+    utils/goldens.py) — on the GPU as one domain and as 8 overlapped x slabs."""
+    it, err, norm = h3d.utils.golden(513, 1e-3)
+    kw = dict(virtual_ranks=vr, decomp=(vr, 1, 1)) if vr > 1 else {}
+    s, r = _solve(h3d, 513, 1e-3, **kw)
+    assert r["converged"] and r["conv_iter"] == it, r
+    assert abs(r["error_percent"] - err) < 6e-5 and abs(r["norm"] - norm) < 1e-6, r
+
+
 def test_hbm_preflight(h3d, gpu):
     """planned_bytes is what the solver takes from HBM (hipMemGetInfo before /
     after), and a configuration that cannot fit is refused before allocating:

@@ -210,6 +210,26 @@ def test_checkpoint_crash_safety_and_checksum(h3d, tmp_path):
         h3d.HeatSolver((19, 17, 21), 60, 0.0, backend="cpu", extra_args=["--restart", str(ck)]).run()
 
 
+def test_checkpoint_interrupted_save_cleaned(h3d, tmp_path):
+    """A save that a crash interrupted leaves a full-grid field.<iter>.raw.tmp
+    behind; the next successful save removes it, and meta.json
+    never pointed at it, so a restart in between resumes the previous save."""
+    import json
+
+    ck = tmp_path / "ck"
+    a = h3d.HeatSolver((19, 17, 21), 40, 0.0, backend="cpu", virtual_ranks=2)
+    a.run()
+    a.save_checkpoint(str(ck))
+    (ck / "field.45.raw.tmp").write_bytes(b"\0" * 1000)  # the crash mid-save at iteration 45
+    assert json.loads((ck / "meta.json").read_text())["field"] == "field.40.raw"
+    b = h3d.HeatSolver((19, 17, 21), 40, 0.0, backend="cpu", extra_args=["--restart", str(ck)])
+    b.initialize()
+    assert b.state()["iter"] == 40
+    a.step(9)
+    a.save_checkpoint(str(ck))
+    assert sorted(p.name for p in ck.iterdir()) == ["field.49.raw", "meta.json"]
+
+
 def test_streamed_io_bounded_chunks(h3d, tmp_path):
     """With a 1 MiB staging chunk the checkpoint, the per-rank Tecplot zones
     and the root gather stream in many chunks and give the same bytes."""

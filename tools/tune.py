@@ -20,6 +20,9 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--shape", type=int, nargs=3, default=None,
+                    help="owned box X Y Z instead of (n-2)^3, e.g. 122 1022 1022 for the interior of the "
+                         "8-GPU slab share of 1024^3")
     ap.add_argument("--dtype", default="fp64")
     ap.add_argument("--variants", nargs="+", default=["tl3"])
     ap.add_argument("--iters", type=int, default=10)
@@ -34,11 +37,11 @@ def main():
     from heat3d_amd import ops
 
     dt = torch.float64 if a.dtype == "fp64" else torch.float32
-    n = (a.n - 2,) * 3
+    n = tuple(a.shape) if a.shape else (a.n - 2,) * 3
     dev = torch.device("cuda", 0)
     f0 = ops.PaddedField(n, dtype=dt, device=dev)
     f1 = ops.PaddedField(n, dtype=dt, device=dev)
-    N = (a.n,) * 3
+    N = tuple(v + 2 for v in n)
     h = tuple(1.0 / (v - 1.0) for v in N)
     ops.init_field(f0, (1, 1, 1), N, h)
     ops.init_field(f1, (1, 1, 1), N, h)
@@ -101,7 +104,7 @@ def main():
     for v in a.variants:
         g = statistics.median(res[v])
         out.append({"variant": v, "glups_median": round(g, 2), "glups_max": round(max(res[v]), 2),
-                    "tbps": round(g * 2 * esize / 1e3, 3), "n": a.n, "dtype": a.dtype})
+                    "tbps": round(g * 2 * esize / 1e3, 3), "n": a.n, "box": list(n), "dtype": a.dtype})
         print(json.dumps(out[-1]), flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:
