@@ -100,8 +100,11 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 }  // namespace
 
 // NTS: store cache policy; SW: swapped axes (x planes are the tile rows, the
-// kernel marches y): the row neighbours are the x terms of the update
-template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
+// kernel marches y): the row neighbours are the x terms of the update; PW:
+// persistent walk (a workgroup loops over several pieces).  PW is its own
+// instantiation: the piece loop costs the single-piece form 8 VGPRs and ~60
+// SGPR spills to VGPR lanes (ROCm 7.2), which the x plan does not need.
+template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false, bool PW = false>
 __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ in, Real* __restrict__ out,
                                                        TBLArgs g, Real Dx, Real Dy, Real Dz,
                                                        unsigned long long* res, const int* done) {
@@ -134,12 +137,12 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
   // tile's contiguous planes; each pays the 2(K-1)-plane pipeline fill).
   //   * x plan (rb >= 0): one piece per block, x segments of `seg` planes
   //     (plan_x: whole rounds of pieces, then a split tail);
-  //   * persistent (rb < 0): exactly as many blocks as the device holds at
+  //   * persistent (PW): exactly as many blocks as the device holds at
   //     once, each a contiguous 1/n1 of the list, so no round of workgroups
   //     is left partly empty and a block only pays a fill where its range
   //     crosses into the next tile.
   int64_t w, wend;
-  if (g.rb < 0) {
+  if (PW) {
     const int64_t W = (int64_t)ntile * nxb;
     const int e = remap(blk, g.n1);
     w = (int64_t)e * W / g.n1;
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     wend = (int64_t)tt * nxb + xhi_p;
   }
 
-  while (w < wend) {
+  do {
   // tile order: z fastest
   const int tt = (int)(w / nxb);
   const int xlo_p = (int)(w - (int64_t)tt * nxb);
@@ -359,8 +362,8 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     residual_commit_block<WY, K>(res, mm, nan_seen,
                                  *reinterpret_cast<unsigned long long(*)[WY][K]>(&s_row[0][0][0][0][0]));
   }
-  if (w < wend) __syncthreads();  // the next piece rewrites the exchange buffer
-  }  // pieces
+  if (PW && w < wend) __syncthreads();  // the next piece rewrites the exchange buffer
+  } while (PW && w < wend);  // pieces
 }
 
 // Tile stride along z.  64 - 2K stored columns per 64-lane tile, or — fp64
@@ -382,19 +385,19 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
   auto cost = [&](int zs) {
     const int64_t tiles = std::max<int64_t>(1, (nz + zs - 1) / zs) * nyb;
     const XPlan p = L > 0 ? fixed_xplan(nx, tiles, L) : plan_x(nx, tiles, slots, 2 * (K - 1), U, L == -1);
-    const double plan = xplan_makespan(p, nx, tiles, slots, 2 * (K - 1), U);
-    if (L != 0 && L != -2) return plan;
-    const double walk = walk_makespan(nx, tiles, slots, 2 * (K - 1), U);
-    return L == -2 ? walk : std::min(plan, walk);
+    if (L == -2) return walk_makespan(nx, tiles, slots, 2 * (K - 1), U);
+    return xplan_makespan(p, nx, tiles, slots, 2 * (K - 1), U);
   };
   constexpr double kAlignedGain = 0.92;
   return cost(aligned) * kAlignedGain < cost(wide) ? aligned : wide;
 }
 
-template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
+// WALK: the persistent-walk instantiation exists for this shape (the default
+// shapes); otherwise only the x plan runs
+template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false, bool WALK = false>
 static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   constexpr bool swap_xy = SW;
-  const void* kfn = reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW>);
+  const void* kfn = reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW, false>);
   Box b = p.box;
   constexpr int TY = WY * R;
   // swap_xy: march along y with x as the tile rows (thin x slabs: a tile of
@@ -458,12 +461,19 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   const int cus = device_cus();
   const int live = std::max(1, (int)((int64_t)slots * std::max(1, cus - p.cu_reserved) / std::max(1, cus)));
   // spec field L: > 0 fixed segments, -1 equal segments, -2 persistent walk,
-  // -3 the x plan, 0 the cheaper of the x plan and the walk in one makespan model
+  // 0 / -3 the x plan
   const XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L)
                             : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L == -1);
   const double plan_cost = xplan_makespan(xp, nxb, ntiles, slots, 2 * (K - 1), U);
   const double walk_cost = walk_makespan(nxb, ntiles, live, 2 * (K - 1), U);
-  const bool walk = ks.L == -2 || (ks.L == 0 && walk_cost < 0.97 * plan_cost);
+  HEAT3D_CHECK(WALK || ks.L != -2, "tl variant " << ks.str() << " has no persistent-walk form");
+  // The walk is opt-in (L = -2): its makespan model wins on every box here,
+  // but MI355X measures it 18-22% slower than the x plan (1024^3 fp64 677 vs
+  // 822 GLUPS, 128 x 1022^2 563 vs 721, 256 x 1022^2 582 vs 706; round 3).
+  // The x plan's concurrent workgroups sweep neighbouring tiles over the same
+  // x planes, so the overlapping halo columns and rows of a tile are L2 hits;
+  // a walk's workgroups sit at unrelated x offsets of their tiles.
+  const bool walk = WALK && ks.L == -2;
   int64_t nblocks;
   if (walk) {
     g.segsplit = 0;
@@ -483,15 +493,27 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
                  K, (long long)nxb, walk ? "walk" : "plan", xp.seg, g.nzb, g.nyb, (long long)nblocks, plan_cost,
                  walk_cost);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl: residual slots " << p.slot << "+" << K);
-  static const int spill = [kfn] {
+  auto scratch = [](const void* f) {
     hipFuncAttributes a{};
-    return hipFuncGetAttributes(&a, kfn) == hipSuccess ? (int)a.localSizeBytes : 0;
-  }();
+    return hipFuncGetAttributes(&a, f) == hipSuccess ? (int)a.localSizeBytes : 0;
+  };
+  static const int spill = scratch(kfn);
   // a spilling variant is refused (one was miscompiled on ROCm 7.2)
   HEAT3D_CHECK(spill == 0, "tl variant " << ks.str() << " spills " << spill << " B of registers per lane");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
-  hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+  if constexpr (WALK) {
+    if (walk) {
+      static const int spill_w = scratch(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>));
+      HEAT3D_CHECK(spill_w == 0, "tl walk variant " << ks.str() << " spills " << spill_w << " B per lane");
+      hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>), dim3((unsigned)nblocks), dim3(64 * WY), 0,
+                         s, static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0],
+                         (Real)p.D[1], (Real)p.D[2], r, done);
+      HIPK_CHECK(hipGetLastError());
+      return;
+    }
+  }
+  hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, false>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
                      static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0], (Real)p.D[1],
                      (Real)p.D[2], r, done);
   HIPK_CHECK(hipGetLastError());
@@ -529,14 +551,17 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
     return true;                                                   \
   }
   // output-store cache-policy bits (spec field 7: 2 = nt, 1 / 16 = sc0 / sc1), default shapes only
-#define H3D_TBLA(RR, YY, KK, AA)                                      \
-  if (R == RR && WY == YY && K == KK && Q == 3 && r.O == (AA)) {      \
-    if (p) launch_tbl<Real, RR, YY, KK, 3, (AA)>(*p, k, s);           \
-    return true;                                                      \
+#define H3D_TBLA(RR, YY, KK, AA, WW)                                    \
+  if (R == RR && WY == YY && K == KK && Q == 3 && r.O == (AA)) {        \
+    if (p) launch_tbl<Real, RR, YY, KK, 3, (AA), false, WW>(*p, k, s);  \
+    return true;                                                        \
   }
-  H3D_TBLA(3, 16, 3, 2) H3D_TBLA(3, 16, 3, 3) H3D_TBLA(3, 16, 3, 17) H3D_TBLA(3, 16, 3, 18) H3D_TBLA(3, 16, 3, 19)
-  H3D_TBLA(2, 16, 4, 2)  // the K = 4 default (long sweeps)
-  H3D_TBLA(3, 12, 4, 2) H3D_TBLA(4, 12, 4, 2)  // 12-wave K = 4 tiles (36 / 48 rows)
+  // the default shapes carry the persistent-walk form
+  H3D_TBLA(3, 16, 3, 2, true) H3D_TBLA(3, 16, 3, 3, false) H3D_TBLA(3, 16, 3, 17, false)
+  H3D_TBLA(3, 16, 3, 18, false) H3D_TBLA(3, 16, 3, 19, false)
+  H3D_TBLA(2, 16, 4, 2, false)
+  H3D_TBLA(3, 12, 4, 2, true)  // the fp64 K = 4 default (long sweeps: 12 waves, 36 rows)
+  H3D_TBLA(4, 12, 4, 2, false)
 #undef H3D_TBLA
   // 16 waves (<= 128 VGPRs, LDS 2K x 16 KiB): K <= 4; 12 waves (<= 168 VGPRs): K = 5
   H3D_TBL(3, 16, 4, 3) H3D_TBL(3, 16, 4, 4) H3D_TBL(3, 16, 3, 3) H3D_TBL(3, 16, 3, 4)
