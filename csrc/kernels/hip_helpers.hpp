@@ -166,6 +166,8 @@ XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_o
 XPlan fixed_xplan(int64_t nx, int64_t tiles, int seg);
 // Makespan of a plan in the same greedy-dispatch model (plane steps per slot).
 double xplan_makespan(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fill, int U);
+// A tiling's sweep cost for the z-stride choice: max(makespan, work / HBM-saturating slots)
+double tiling_cost(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fill, int U);
 // Same model for the persistent walk: `live` workgroups, each a contiguous
 // 1/live of the tile-major (tile, plane) list, a fill per tile it touches.
 double walk_makespan(int64_t nx, int64_t tiles, int live, int fill, int U);

@@ -32,6 +32,7 @@ struct KernelSpec {
   int L = 0;  // x-segment length per wave (0 = auto)
   int O = -1; // TBL: output-store cache-policy bits (2 = nt)
   int NT = 0; // TBL: T^n ring size
+  int ZS = 0; // TBL: tile stride along z (stored columns per tile; 0 = chosen per box)
   bool multi_step() const { return kind == TBL; }
   static KernelSpec parse(const std::string& s);
   std::string str() const;

@@ -350,6 +350,19 @@ double xplan_makespan(const XPlan& p, int64_t nx, int64_t tiles, int slots, int 
   return simulate_xplan(p, nx, tiles, slots, fill, U, heap);
 }
 
+// Sweep time of a tiling in plane-steps per slot: the greedy-dispatch
+// makespan, but never less than the total work spread over the workgroups
+// that saturate HBM (~80% of the slots: tools/probes/tile_probe.hip, 176 of
+// 256 workgroups already moved 5.45 TB/s).  The makespan alone sees no cost
+// in a tile column that is almost empty as long as every tile still fits one
+// round of workgroups — but the sweep is bandwidth-bound, so that column's
+// loads are paid for: fp32 1022^3 with 112-column pair tiles (10 columns,
+// the last 14 wide) ran 1294 GLUPS against 1397 with 120 (9 columns).
+double tiling_cost(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fill, int U) {
+  const double work = (double)tiles * (double)(nx + fill) / (0.8 * std::max(1, slots));
+  return std::max(xplan_makespan(p, nx, tiles, slots, fill, U), work);
+}
+
 XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_only) {
   struct Key {
     int64_t nx, tiles;

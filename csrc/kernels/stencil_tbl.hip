@@ -386,7 +386,7 @@ int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, 
     const int64_t tiles = std::max<int64_t>(1, (nz + zs - 1) / zs) * nyb;
     const XPlan p = L > 0 ? fixed_xplan(nx, tiles, L) : plan_x(nx, tiles, slots, 2 * (K - 1), U, L == -1);
     if (L == -2) return walk_makespan(nx, tiles, slots, 2 * (K - 1), U);
-    return xplan_makespan(p, nx, tiles, slots, 2 * (K - 1), U);
+    return tiling_cost(p, nx, tiles, slots, 2 * (K - 1), U);
   };
   constexpr double kAlignedGain = 0.92;
   return cost(aligned) * kAlignedGain < cost(wide) ? aligned : wide;
@@ -448,7 +448,9 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   constexpr int YS = TY - 2 * K;
   static const int slots = device_slots(kfn, 64 * WY);  // magic static: thread-safe under --gpus N
   constexpr int U = Q == 4 ? 12 : 6;  // the kernel's unroll (lcm(Q, 3, 2))
-  const int ZS = lean_z_stride(b.extent(0), b.extent(1), b.extent(2), K, (int)sizeof(Real), TY, slots, U, ks.L);
+  const int ZS = ks.ZS > 0 ? ks.ZS
+                           : lean_z_stride(b.extent(0), b.extent(1), b.extent(2), K, (int)sizeof(Real), TY, slots, U, ks.L);
+  HEAT3D_CHECK(ZS >= 1 && ZS <= 64 - 2 * K, "tl: z stride " << ZS << " outside [1, " << 64 - 2 * K << "]");
   g.zs = ZS;
   g.c00 = (int)(b.lo[2] - K);
   g.r00 = (int)(b.lo[1] - K);

@@ -308,10 +308,12 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
 // Tile stride along z: 128 - 2K - 2 stored columns (tiles start on even
 // columns), or the largest multiple of 16 below it, which starts every tile's
 // stored strip on a 64-byte boundary (whole 64-B write segments at both
-// seams; 2049^3 fp32 1513 -> 1552 GLUPS with 112 instead of 120, round 2).
+// seams; 2049^3 fp32 1456 -> 1531 GLUPS with 112 instead of 120, round 3).
 // The narrower stride can add a tile column, so — as lean_z_stride does for
-// fp64 — it is taken only where the x-plan model, with that gain, predicts a
-// shorter sweep, and only for boxes of >= 500 x planes.
+// fp64 — it is taken only where the tiling cost (tiling_cost), with that
+// gain, predicts a shorter sweep, and only for boxes of >= 500 x planes
+// (1022^3: 120 keeps 9 tile columns, 112 would add a 14-wide 10th: 1397 vs
+// 1294 GLUPS).
 int pair_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L) {
   const int wide = 128 - 2 * K - 2;
   const int aligned = wide & ~15;
@@ -320,7 +322,7 @@ int pair_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, 
   auto cost = [&](int zs) {
     const int64_t tiles = std::max<int64_t>(1, (nz + zs - 1) / zs) * nyb;
     const XPlan p = L > 0 ? fixed_xplan(nx, tiles, L) : plan_x(nx, tiles, slots, 2 * (K - 1), U, L < 0);
-    return xplan_makespan(p, nx, tiles, slots, 2 * (K - 1), U);
+    return tiling_cost(p, nx, tiles, slots, 2 * (K - 1), U);
   };
   constexpr double kAlignedGain = 0.92;
   return cost(aligned) * kAlignedGain < cost(wide) ? aligned : wide;
@@ -371,7 +373,9 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   static const int slots =  // magic static: thread-safe under --gpus N
       device_slots(reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q, AUX>), 64 * WY);
   constexpr int U = Q == 4 ? 12 : 6;
-  const int ZS = pair_z_stride(b.extent(0), b.extent(1), b.extent(2), K, TY, slots, U, ks.L);
+  const int ZS = ks.ZS > 0 ? ks.ZS : pair_z_stride(b.extent(0), b.extent(1), b.extent(2), K, TY, slots, U, ks.L);
+  HEAT3D_CHECK(ZS >= 2 && ZS % 2 == 0 && ZS <= 128 - 2 * K - 2,
+               "tl pair: z stride " << ZS << " must be even and in [2, " << 128 - 2 * K - 2 << "]");
   g.zs = ZS;
   constexpr int YS = TY - 2 * K;
   g.r00 = (int)(b.lo[1] - K);

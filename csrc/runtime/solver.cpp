@@ -76,12 +76,13 @@ KernelSpec KernelSpec::parse(const std::string& s) {
     k.L = at(5);
     k.NT = at(6);
     if (k.kind != Tile && parts.size() > 7) k.O = at(7);  // store cache-policy bits
+    if (k.kind != Tile && parts.size() > 8) k.ZS = at(8);  // z tile stride
   } else if (h == "column" || h == "tb2" || h == "tbk2" || (h.size() == 3 && h[0] == 't' && (h[1] == 'b' || h[1] == 'r'))) {
     throw UsageError("kernel '" + s + "' was retired in round 3 (the column / queue / register-ring kernels); "
                      "use tile for single steps and tl2..tl6 for K-step sweeps");
   } else {
     throw UsageError("unknown kernel '" + s + "' (auto | naive | tile[:V[:R[:WZ[:WY]]]] | "
-                     "tl2..tl6[:V[:R[:WZ[:WY[:L[:Q[:STORE]]]]]]])");
+                     "tl2..tl6[:V[:R[:WZ[:WY[:L[:Q[:STORE[:ZS]]]]]]]])");
   }
   return k;
 }
@@ -148,7 +149,8 @@ std::string KernelSpec::str() const {
   std::ostringstream os;
   os << (kind == Tile ? std::string("tile:") : "tl" + std::to_string(K) + ":") << V << ":" << R << ":" << WZ << ":"
      << WY << ":" << L << ":" << NT;
-  if (kind != Tile && O > 0) os << ":" << O;
+  if (kind != Tile && (O > 0 || ZS > 0)) os << ":" << O;
+  if (kind != Tile && ZS > 0) os << ":" << ZS;
   return os.str();
 }
 
