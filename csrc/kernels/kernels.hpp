@@ -87,6 +87,14 @@ void stencil(DType t, const StencilParams& p, const KernelSpec& k, void* stream)
 void stencil_lean(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
 // z tile stride of the lean kernel for a box (host-side choice, stencil_tbl.hip)
 int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U, int L);
+// The x plan the sweep kernels would take for a box of nx planes and `tiles`
+// tiles on `slots` resident workgroups (seg > 0: fixed segments, -1: equal
+// segments, 0: auto), with its greedy-dispatch makespan in plane steps
+struct XPlanInfo {
+  int seg = 1, n1 = 0, r = 0, split = 0, nb2 = 0;
+  double makespan = 0;
+};
+XPlanInfo describe_xplan(int64_t nx, int64_t tiles, int slots, int fill, int U, int seg);
 // fp32 lean kernel on packed pairs of z columns (stencil_tbp.hip; spec tlK:2:…)
 void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream);
 bool lean_pair_supported(const KernelSpec& k);

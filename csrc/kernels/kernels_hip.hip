@@ -418,6 +418,18 @@ XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_o
   return best;
 }
 
+XPlanInfo describe_xplan(int64_t nx, int64_t tiles, int slots, int fill, int U, int seg) {
+  const XPlan p = seg > 0 ? fixed_xplan(nx, tiles, seg) : plan_x(nx, tiles, slots, fill, U, seg == -1);
+  XPlanInfo d;
+  d.seg = p.seg;
+  d.n1 = p.n1;
+  d.r = p.r;
+  d.split = p.split;
+  d.nb2 = p.nb2;
+  d.makespan = xplan_makespan(p, nx, tiles, slots, fill, U);
+  return d;
+}
+
 template <typename Real, int V, int R, int WZ, int WY>
 static void launch_tile(const StencilParams& p, const KernelSpec& k, hipStream_t s) {
   const Box& b = p.box;

@@ -173,6 +173,19 @@ PYBIND11_MODULE(_heat3d, m) {
   m.def("lean_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U) {
     return heat3d::hip::lean_z_stride(nx, ny, nz, K, esize, TY, slots, U, 0);
   });
+  // the x plan of a sweep and its modelled makespan (plane steps per slot)
+  m.def("x_plan", [](int64_t nx, int64_t tiles, int slots, int fill, int U, int seg) {
+    const heat3d::hip::XPlanInfo p = heat3d::hip::describe_xplan(nx, tiles, slots, fill, U, seg);
+    py::dict d;
+    d["seg"] = p.seg;
+    d["n1"] = p.n1;
+    d["r"] = p.r;
+    d["split"] = p.split;
+    d["nb2"] = p.nb2;
+    d["makespan"] = p.makespan;
+    d["ideal"] = (double)tiles * (double)(nx + fill) / slots;
+    return d;
+  }, py::arg("nx"), py::arg("tiles"), py::arg("slots"), py::arg("fill"), py::arg("U"), py::arg("seg") = 0);
   m.def("pair_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U) {
     return heat3d::hip::pair_z_stride(nx, ny, nz, K, TY, slots, U, 0);
   });
