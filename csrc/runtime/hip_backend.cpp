@@ -153,6 +153,13 @@ class HipBackend final : public Backend {
     const int words = (cus + 31) / 32;
     std::vector<uint32_t> mask(words, 0u);
     for (int i = 0; i < cus - n; ++i) mask[i / 32] |= 1u << (i % 32);  // clear the top n bits
+    // Mask bit i is a CU of XCD i mod 8 (measured: tests/test_gpu_placement.py),
+    // so the top n = 8 bits keep one CU per XCD free.  HIP offers no flags
+    // or priority for a CU-masked stream: it is a blocking stream of normal
+    // priority (the stream it replaces was non-blocking, lowest priority).
+    // The comm / reduce streams keep their higher priority, and no solver
+    // work is issued to the legacy null stream, so neither difference
+    // orders anything the solver issues.
     hipStream_t s = nullptr;
     HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask.data()));
     HIP_CHECK(hipStreamSynchronize(streams_[kCompute]));

@@ -73,6 +73,16 @@ def test_bench_self_launch_rccl(gpu, tmp_path):
     assert j["n_gpus"] == 2 and j["comm_ranks"] == 2 and j["halo_verified"]
     assert j["config"]["comm"] == "rccl" and j["config"]["parallelism"] == "slab 2x1x1"
     assert j["value"] > 0 and j["steps"] == 6 and [q["rank"] for q in j["placement"]] == [0, 1]
+    # the per-rank phase block the N-GPU JSON carries:
+    # every rank reports its overlapped schedule's phases per sweep
+    ph = j["phases"]
+    assert [q["rank"] for q in ph] == [0, 1], ph
+    for q in ph:
+        for key in ("interior_ms", "halo_ms", "boundary_ms", "allreduce_ms", "check_ms", "compute_idle_ms",
+                    "sweep_ms", "chain_overlap_fraction"):
+            assert key in q, (key, q)
+        assert q["sweeps"] > 0 and q["steps_per_sweep"] == 3 and q["interior_ms"] > 0 and q["halo_ms"] > 0
+        assert 0.0 <= q["chain_overlap_fraction"] <= 1.0 and q["sweep_ms"] >= q["interior_ms"] * 0.5, q
 
 
 def test_bench_self_launch_socket(gpu, tmp_path):
