@@ -252,8 +252,11 @@ def run_rank(args) -> int:
     K = s.native.temporal_steps
     nbuf = s.native.field_buffers
     reserved = s.native.reserved_cus
+    # the x schedules timed at start-up (Config autotune): L = -3 is the
+    # dispatch model's plan, L > 0 fixed x segments of L planes
+    xs = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in t.items()} for t in ext.tuned_schedules()]
     placement = all_gather_objects({"rank": rank, "device": dev, "host": socket.gethostname(),
-                                    "subdomain": list(s.native.local_subdomain(0)["n"])}, group)
+                                    "subdomain": list(s.native.local_subdomain(0)["n"]), "x_schedules": xs}, group)
     # per-rank schedule profile, after (outside) the timed window: a few more
     # sweeps of the same pipeline with timing events at its phase boundaries
     # (interior / halo / boundary / all-reduce / check, compute-stream idle,

@@ -174,5 +174,18 @@ double walk_makespan(int64_t nx, int64_t tiles, int live, int fill, int U);
 // Compute units of the current device (cached per device).
 int device_cus();
 
+// x-schedule autotuning (round 3).  The dispatch model above picks the best
+// measured segment on the 1022^3 boxes but not on every box (the 2-GPU slab
+// share's interior, 506 x 1022^2: whole tiles 772 GLUPS, 2 segments 812;
+// profiles/xplan_calibration_r03.md), so a sweep shape can be timed once:
+// tune_x_schedule launches every candidate value of spec field L (-3 = the
+// model's x plan, > 0 fixed segments of nx/k planes) twice on `s`, keeps the
+// fastest (the model's plan unless another is >= 1.5% faster) per (device,
+// kernel, nx, tiles, slots, reserved CUs) and returns it; tuned_x_lookup
+// returns a kept choice or 0.
+int tuned_x_lookup(const void* kfn, int64_t nx, int64_t tiles, int slots, int reserved);
+int tune_x_schedule(const char* name, const void* kfn, int64_t nx, int64_t tiles, int slots, int reserved, int U,
+                    hipStream_t s, const std::function<void(int)>& launch);
+
 }  // namespace hip
 }  // namespace heat3d

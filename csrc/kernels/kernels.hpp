@@ -10,6 +10,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../core/common.hpp"
 #include "layout.hpp"
@@ -59,6 +60,10 @@ struct StencilParams {
   // CUs the launch stream's CU mask keeps free (persistent sweeps launch as
   // many workgroups as the remaining CUs hold)
   int cu_reserved = 0;
+  // sweeps only: time the x-schedule candidates on this launch (a sweep is
+  // idempotent: every candidate writes the same T^{n+K} to out) and keep the
+  // fastest for this kernel and box shape (autotune_x_schedule)
+  bool tune = false;
 };
 
 struct InitParams {
@@ -95,6 +100,18 @@ struct XPlanInfo {
   double makespan = 0;
 };
 XPlanInfo describe_xplan(int64_t nx, int64_t tiles, int slots, int fill, int U, int seg);
+
+// x schedules chosen by timing (StencilParams::tune): kernel, box planes,
+// tiles, the winning spec-field-L value (-3 = the model's x plan, > 0 fixed
+// segments) and the measured ms of the winner and of the model's plan
+struct TunedSchedule {
+  std::string kernel;
+  int64_t nx = 0, tiles = 0;
+  int L = 0;
+  double ms = 0, ms_model = 0;
+  int candidates = 0;
+};
+std::vector<TunedSchedule> tuned_schedules();
 // fp32 lean kernel on packed pairs of z columns (stencil_tbp.hip; spec tlK:2:…)
 void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream);
 bool lean_pair_supported(const KernelSpec& k);

@@ -418,6 +418,99 @@ XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_o
   return best;
 }
 
+namespace {
+struct TuneKey {
+  int dev;
+  const void* kfn;
+  int64_t nx, tiles;
+  int slots, reserved;
+  bool operator<(const TuneKey& o) const {
+    return std::tie(dev, kfn, nx, tiles, slots, reserved) < std::tie(o.dev, o.kfn, o.nx, o.tiles, o.slots, o.reserved);
+  }
+};
+std::mutex tune_mu;
+std::map<TuneKey, TunedSchedule> tune_cache;
+}  // namespace
+
+int tuned_x_lookup(const void* kfn, int64_t nx, int64_t tiles, int slots, int reserved) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(tune_mu);
+  auto it = tune_cache.find(TuneKey{dev, kfn, nx, tiles, slots, reserved});
+  return it == tune_cache.end() ? 0 : it->second.L;
+}
+
+int tune_x_schedule(const char* name, const void* kfn, int64_t nx, int64_t tiles, int slots, int reserved, int U,
+                    hipStream_t s, const std::function<void(int)>& launch) {
+  int dev = 0;
+  HIPK_CHECK(hipGetDevice(&dev));
+  const TuneKey key{dev, kfn, nx, tiles, slots, reserved};
+  {
+    std::unique_lock<std::mutex> lk(tune_mu);
+    auto it = tune_cache.find(key);
+    if (it != tune_cache.end()) {
+      const int L = it->second.L;
+      lk.unlock();
+      launch(L);
+      return L;
+    }
+  }
+  // candidates: the model's plan, then segments of nx / k planes (distinct,
+  // >= one unrolled chunk, not the model's own segment)
+  std::vector<int> cand{-3};
+  for (int k : {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16}) {
+    const int seg = (int)((nx + k - 1) / k);
+    if (seg < U || seg >= (1 << 15)) continue;
+    if (std::find(cand.begin(), cand.end(), seg) != cand.end()) continue;
+    cand.push_back(seg);
+  }
+  hipEvent_t e0, e1;
+  HIPK_CHECK(hipEventCreate(&e0));
+  HIPK_CHECK(hipEventCreate(&e1));
+  std::vector<float> best(cand.size(), 1e30f);
+  launch(-3);  // warm: code object, caches, clocks
+  for (int rep = 0; rep < 2; ++rep) {
+    for (std::size_t i = 0; i < cand.size(); ++i) {
+      HIPK_CHECK(hipEventRecord(e0, s));
+      launch(cand[i]);
+      HIPK_CHECK(hipEventRecord(e1, s));
+      HIPK_CHECK(hipEventSynchronize(e1));
+      float ms = 0;
+      HIPK_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      best[i] = std::min(best[i], ms);
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  std::size_t w = 0;
+  for (std::size_t i = 1; i < cand.size(); ++i)
+    if (best[i] < best[w]) w = i;
+  if (best[w] > best[0] / 1.015f) w = 0;  // ties go to the model's plan
+  TunedSchedule t;
+  t.kernel = name;
+  t.nx = nx;
+  t.tiles = tiles;
+  t.L = cand[w];
+  t.ms = best[w];
+  t.ms_model = best[0];
+  t.candidates = (int)cand.size();
+  if (std::getenv("HEAT3D_TRACE")) {
+    std::fprintf(stderr, "[heat3d trace] x-schedule %s nx=%lld tiles=%lld:", name, (long long)nx, (long long)tiles);
+    for (std::size_t i = 0; i < cand.size(); ++i) std::fprintf(stderr, " %d:%.3f", cand[i], best[i]);
+    std::fprintf(stderr, " -> %d\n", t.L);
+  }
+  std::lock_guard<std::mutex> lk(tune_mu);
+  tune_cache[key] = t;
+  return t.L;
+}
+
+std::vector<TunedSchedule> tuned_schedules() {
+  std::lock_guard<std::mutex> lk(tune_mu);
+  std::vector<TunedSchedule> v;
+  for (auto& kv : tune_cache) v.push_back(kv.second);
+  return v;
+}
+
 XPlanInfo describe_xplan(int64_t nx, int64_t tiles, int slots, int fill, int U, int seg) {
   const XPlan p = seg > 0 ? fixed_xplan(nx, tiles, seg) : plan_x(nx, tiles, slots, fill, U, seg == -1);
   XPlanInfo d;

@@ -462,12 +462,6 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   // are not there for the persistent walk)
   const int cus = device_cus();
   const int live = std::max(1, (int)((int64_t)slots * std::max(1, cus - p.cu_reserved) / std::max(1, cus)));
-  // spec field L: > 0 fixed segments, -1 equal segments, -2 persistent walk,
-  // 0 / -3 the x plan
-  const XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L)
-                            : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L == -1);
-  const double plan_cost = xplan_makespan(xp, nxb, ntiles, slots, 2 * (K - 1), U);
-  const double walk_cost = walk_makespan(nxb, ntiles, live, 2 * (K - 1), U);
   HEAT3D_CHECK(WALK || ks.L != -2, "tl variant " << ks.str() << " has no persistent-walk form");
   // The walk is opt-in (L = -2): its makespan model wins on every box here,
   // but MI355X measures it 18-22% slower than the x plan (1024^3 fp64 677 vs
@@ -476,24 +470,6 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   // x planes, so the overlapping halo columns and rows of a tile are L2 hits;
   // a walk's workgroups sit at unrelated x offsets of their tiles.
   const bool walk = WALK && ks.L == -2;
-  int64_t nblocks;
-  if (walk) {
-    g.segsplit = 0;
-    g.n1 = (int)std::min<int64_t>(live, ntiles * nxb);
-    g.rb = -1;
-    nblocks = g.n1;
-  } else {
-    HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
-    g.segsplit = xp.seg | (xp.split << 16);
-    g.n1 = xp.n1;
-    g.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
-    nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
-  }
-  HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
-  if (std::getenv("HEAT3D_TRACE"))
-    std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: %s seg=%d tiles=%dx%d blocks=%lld (plan %.1f walk %.1f)\n",
-                 K, (long long)nxb, walk ? "walk" : "plan", xp.seg, g.nzb, g.nyb, (long long)nblocks, plan_cost,
-                 walk_cost);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl: residual slots " << p.slot << "+" << K);
   auto scratch = [](const void* f) {
     hipFuncAttributes a{};
@@ -506,19 +482,53 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   const int* done = p.state ? &p.state->done : nullptr;
   if constexpr (WALK) {
     if (walk) {
+      g.segsplit = 0;
+      g.n1 = (int)std::min<int64_t>(live, ntiles * nxb);
+      g.rb = -1;
       static const int spill_w = scratch(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>));
       HEAT3D_CHECK(spill_w == 0, "tl walk variant " << ks.str() << " spills " << spill_w << " B per lane");
-      hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>), dim3((unsigned)nblocks), dim3(64 * WY), 0,
-                         s, static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0],
-                         (Real)p.D[1], (Real)p.D[2], r, done);
+      if (std::getenv("HEAT3D_TRACE"))
+        std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: walk tiles=%dx%d blocks=%d\n", K, (long long)nxb,
+                     g.nzb, g.nyb, g.n1);
+      hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>), dim3((unsigned)g.n1), dim3(64 * WY), 0, s,
+                         static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0], (Real)p.D[1],
+                         (Real)p.D[2], r, done);
       HIPK_CHECK(hipGetLastError());
       return;
     }
   }
-  hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, false>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
-                     static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0], (Real)p.D[1],
-                     (Real)p.D[2], r, done);
-  HIPK_CHECK(hipGetLastError());
+  // spec field L: > 0 fixed segments, -1 equal segments, -2 persistent walk,
+  // -3 the x plan; 0: the schedule timed for this shape (tune_x_schedule),
+  // else the x plan
+  auto fire = [&](int Lx) {
+    TBLArgs ga = g;
+    const XPlan xp = Lx > 0 ? fixed_xplan(nxb, ntiles, Lx) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, Lx == -1);
+    HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
+    ga.segsplit = xp.seg | (xp.split << 16);
+    ga.n1 = xp.n1;
+    ga.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
+    const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
+    HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
+    if (std::getenv("HEAT3D_TRACE"))
+      std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: L=%d seg=%d tiles=%dx%d blocks=%lld (model %.1f)\n",
+                   K, (long long)nxb, Lx, xp.seg, g.nzb, g.nyb, (long long)nblocks,
+                   xplan_makespan(xp, nxb, ntiles, slots, 2 * (K - 1), U));
+    hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, false>), dim3((unsigned)nblocks), dim3(64 * WY), 0,
+                       s, static_cast<const Real*>(p.in), static_cast<Real*>(p.out), ga, (Real)p.D[0], (Real)p.D[1],
+                       (Real)p.D[2], r, done);
+    HIPK_CHECK(hipGetLastError());
+  };
+  if (ks.L == 0 && !SW) {
+    if (p.tune) {
+      tune_x_schedule(SW ? "tl-y" : sizeof(Real) == 8 ? "tl-fp64" : "tl-fp32", kfn, nxb, ntiles, slots,
+                      p.cu_reserved, U, s, fire);
+      return;  // every candidate computed this sweep
+    }
+    const int t = tuned_x_lookup(kfn, nxb, ntiles, slots, p.cu_reserved);
+    fire(t != 0 ? t : 0);
+    return;
+  }
+  fire(ks.L);
 }
 
 // p == nullptr: only report whether the variant k resolves to exists

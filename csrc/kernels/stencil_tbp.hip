@@ -383,13 +383,6 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
   const int64_t ntiles = (int64_t)g.nzb * g.nyb;
   const int64_t nxb = b.extent(0);
-  XPlan xp = ks.L > 0 ? fixed_xplan(nxb, ntiles, ks.L) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, ks.L < 0);
-  HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl pair: x plan out of range");
-  g.segsplit = xp.seg | (xp.split << 16);
-  g.n1 = xp.n1;
-  g.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
-  const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
-  HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl pair: bad block count " << nblocks);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl pair: residual slots " << p.slot << "+" << K);
   static const int spill = [] {
     hipFuncAttributes a{};
@@ -400,10 +393,32 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(spill == 0, "tl pair variant " << ks.str() << " spills " << spill << " B of registers per lane");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
-  hipLaunchKernelGGL((stencil_tbp<R, WY, K, Q, AUX>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
-                     static_cast<const float*>(p.in), static_cast<float*>(p.out), g, (float)p.D[0], (float)p.D[1],
-                     (float)p.D[2], r, done);
-  HIPK_CHECK(hipGetLastError());
+  // spec field L as in launch_tbl (0: the timed schedule of this shape, else the x plan)
+  auto fire = [&](int Lx) {
+    TBPArgs ga = g;
+    const XPlan xp = Lx > 0 ? fixed_xplan(nxb, ntiles, Lx) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, Lx == -1);
+    HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl pair: x plan out of range");
+    ga.segsplit = xp.seg | (xp.split << 16);
+    ga.n1 = xp.n1;
+    ga.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
+    const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
+    HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl pair: bad block count " << nblocks);
+    hipLaunchKernelGGL((stencil_tbp<R, WY, K, Q, AUX>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+                       static_cast<const float*>(p.in), static_cast<float*>(p.out), ga, (float)p.D[0], (float)p.D[1],
+                       (float)p.D[2], r, done);
+    HIPK_CHECK(hipGetLastError());
+  };
+  const void* kfn = reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q, AUX>);
+  if (ks.L == 0) {
+    if (p.tune) {
+      tune_x_schedule("tl-fp32-pair", kfn, nxb, ntiles, slots, p.cu_reserved, U, s, fire);
+      return;
+    }
+    const int t = tuned_x_lookup(kfn, nxb, ntiles, slots, p.cu_reserved);
+    fire(t != 0 ? t : 0);
+    return;
+  }
+  fire(ks.L);
 }
 
 // p == nullptr: only report whether the variant k resolves to exists

@@ -186,6 +186,22 @@ PYBIND11_MODULE(_heat3d, m) {
     d["ideal"] = (double)tiles * (double)(nx + fill) / slots;
     return d;
   }, py::arg("nx"), py::arg("tiles"), py::arg("slots"), py::arg("fill"), py::arg("U"), py::arg("seg") = 0);
+  // x schedules chosen by timing at solver start-up (Config::autotune)
+  m.def("tuned_schedules", []() {
+    py::list out;
+    for (const auto& t : heat3d::hip::tuned_schedules()) {
+      py::dict d;
+      d["kernel"] = t.kernel;
+      d["nx"] = t.nx;
+      d["tiles"] = t.tiles;
+      d["L"] = t.L;
+      d["ms"] = t.ms;
+      d["ms_model"] = t.ms_model;
+      d["candidates"] = t.candidates;
+      out.append(d);
+    }
+    return out;
+  });
   m.def("pair_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U) {
     return heat3d::hip::pair_z_stride(nx, ny, nz, K, TY, slots, U, 0);
   });

@@ -444,6 +444,7 @@ void Solver::initialize() {
       be_->init_field(dt_, p, kCompute);
     }
   }
+  tune_schedules();
   DeviceState hs;
   std::memset(&hs, 0, sizeof(hs));
   for (auto& r : hs.residual) r = kResidualInitBits;
@@ -471,6 +472,47 @@ void Solver::initialize() {
   }
   be_->sync_all();
   comm_->barrier(*be_);
+}
+
+// Time the x-schedule candidates of every interior sweep shape this run will
+// launch (hip::tune_x_schedule) before the first iteration, on the freshly
+// initialised fields: each candidate computes sweep 0 of the interior box
+// into the next buffer without residual state, which the first real sweep
+// overwrites with the same values.  The chosen schedules then serve every
+// eager launch and every graph capture of the run.
+void Solver::tune_schedules() {
+  if (!cfg_.autotune || !tb_ || !be_->is_gpu()) return;
+  std::vector<KernelSpec> specs{kspec2_};
+  if (!has_halo_ && cfg_.long_sweeps && K_ + 1 <= 6 && K_ + 1 <= kResidualSlots) {
+    KernelSpec ks;
+    ks.kind = kspec2_.kind;
+    ks.K = K_ + 1;
+    if (hip::lean_supported(dt_, ks)) specs.push_back(ks);
+  }
+  for (const KernelSpec& ks : specs) {
+    const int Kp = ks.K;
+    for (auto& l : local_) {
+      if (l.tb_interior.empty()) continue;
+      StencilParams sp;
+      sp.in = l.field[0];
+      sp.out = l.field[nxt(0)];
+      sp.L = l.L;
+      sp.box = l.tb_interior;
+      for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+      sp.state = nullptr;
+      sp.cu_reserved = be_->reserved_cus();
+      sp.tune = true;
+      auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
+        o[0] = u[0] < 0 ? -(Kp - 1) : u[0];
+        o[1] = u[1] > n ? n + Kp - 1 : u[1];
+      };
+      shrink(l.ux, l.sd.n[0], sp.ux);
+      shrink(l.uy, l.sd.n[1], sp.uy);
+      shrink(l.uz, l.sd.n[2], sp.uz);
+      be_->sweep(dt_, sp, ks, kCompute);
+    }
+  }
+  be_->sync(kCompute);
 }
 
 // --- one iteration -----------------------------------------------------------

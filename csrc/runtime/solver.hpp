@@ -86,6 +86,8 @@ class Solver {
 
   // (Re)initialise fields: analytic IC/BC (heat3D.cu:408-453) or restart.
   void initialize();
+  // x-schedule autotuning of the interior sweeps (Config::autotune)
+  void tune_schedules();
   // Full solve: iterate until converged or iter_max (heat3D.cu:541-1073).
   RunResult run();
   // Enqueue exactly n iterations without host polling (benchmarks); async.

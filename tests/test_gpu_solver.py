@@ -157,3 +157,27 @@ def test_nan_fault_detected(h3d, gpu):
     s.native.inject(0, 5, 5, 5, float("nan"))
     r = s.run()
     assert r["fault"] and not r["converged"]
+
+
+@pytest.mark.parametrize("vr", [1, 2])
+def test_schedule_autotune_bitwise(h3d, gpu, vr):
+    """Start-up timing of the interior sweeps' x schedules (Solver::tune_schedules,
+    hip::tune_x_schedule): the candidates write the next buffer without residual
+    state, the chosen schedule is kept per kernel and box, and the run is bitwise
+    the run with the dispatch model's schedule (--no-autotune)."""
+    n, iters = (200, 67, 131), 61
+    kw = dict(virtual_ranks=vr, decomp=(vr, 1, 1)) if vr > 1 else {}
+    a = h3d.HeatSolver(n, iters, 0.0, backend="hip", **kw)
+    b = h3d.HeatSolver(n, iters, 0.0, backend="hip", extra_args=["--no-autotune"], **kw)
+    ra, rb = a.run(), b.run()
+    assert ra["iterations"] == rb["iterations"] == iters and ra["last_residual"] == rb["last_residual"]
+    assert np.array_equal(a.gather(), b.gather())
+    tuned = h3d.native().tuned_schedules()
+    # one domain: the 198 interior planes of the 200-point grid; slabs: the
+    # interior of a 99-plane share (the K = 3 planes at the neighbour face are
+    # boundary slabs)
+    mine = [t for t in tuned if t["kernel"] == "tl-fp64" and (t["nx"] == 198 if vr == 1 else 90 <= t["nx"] <= 99)]
+    assert mine, tuned
+    for t in mine:
+        assert t["candidates"] >= 2 and t["ms"] > 0 and t["ms"] <= t["ms_model"] + 1e-9, t
+        assert t["L"] == -3 or t["L"] > 0, t
