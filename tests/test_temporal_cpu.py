@@ -288,3 +288,37 @@ def test_lean_store_policy_defaults(h3d):
     assert r("tl3:1:2:1:16", "fp64") == "tl3:1:2:1:16:0:3"
     assert r("tl3", "fp32") == "tl3:2:3:1:16:0:3:2"
     assert r("tl4", "fp32") == "tl4:2:2:1:16:0:3"
+
+
+def test_pair_z_stride_counts_bytes(h3d):
+    """fp32 pair tiles: the aligned 112-column stride where it does not add a
+    nearly empty tile column (2047^3: 1531 vs 1456 GLUPS), 120 where it would
+    (1022^3: 9 columns of 120 vs 10 of 112, the last 14 wide: 1397 vs 1294) —
+    tiling_cost charges the bytes of every tile, not only the makespan
+    (profiles/xplan_calibration_r03.md)."""
+    zs = lambda n: h3d.native().pair_z_stride(n, n, n, 3, 48, 256, 6)  # noqa: E731
+    assert zs(1022) == 120 and zs(2047) == 112 and zs(4094) == 112
+
+
+def test_x_plan_model(h3d):
+    """The host x planner (binding x_plan): 1022^3 fp64 takes 7 segments of 146
+    planes (3325 pieces = 12.99 rounds of 256, the best measured segment),
+    thin slab shares whole-x pieces, the 4-GPU share a split tail; forced
+    segments are honoured and the model never beats the ideal."""
+    xp = h3d.native().x_plan
+    p = xp(1022, 475, 256, 4, 6)
+    assert p["seg"] == 146 and p["n1"] == 3325 and p["r"] == 0
+    assert xp(122, 450, 256, 4, 6)["seg"] == 122
+    t = xp(250, 450, 256, 4, 6)
+    assert t["n1"] == 256 and t["r"] == 194 and t["nb2"] == 194 and 0 < t["split"] < 250
+    assert xp(1022, 475, 256, 4, 6, 511)["seg"] == 511
+    for nx, tiles in ((1022, 475), (122, 450), (2047, 931), (510, 117)):
+        q = xp(nx, tiles, 256, 4, 6)
+        assert q["makespan"] >= q["ideal"], q
+
+
+def test_kernel_spec_z_stride_field(h3d):
+    """Spec field 9 forces the z tile stride and survives resolution."""
+    r = h3d.native().kernel_spec_resolved
+    assert r("tl3:1:3:1:16:0:3:2:56", "fp64") == "tl3:1:3:1:16:0:3:2:56"
+    assert r("tl3:2:3:1:16:0:3:2:112", "fp32") == "tl3:2:3:1:16:0:3:2:112"
