@@ -64,6 +64,8 @@ def main() -> int:
     dt = time.perf_counter() - t0
     st = s.state()
     assert st["iter"] == args.warmup + args.steps, st
+    # the schedule's phases per sweep (after the timed window, as bench.py's 'phases')
+    phases = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in s.native.profile_sweeps(8).items()}
     out = {"proxy": "phantom rank", "rank": r, "ranks": P, "dims": list(dims), "grid": args.grid,
            "dtype": args.dtype, "gbps": args.gbps, "ar_us": args.ar_us, "extra": args.extra,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "kernel": s.kernel,
@@ -75,7 +77,8 @@ def main() -> int:
            # before the solver's allocations / after initialize()
            "mem_planned_gb": gb(s.native.planned_bytes), "mem_free_before_gb": gb(s.native.mem_free_before),
            "mem_free_after_gb": gb(free_after), "mem_total_gb": gb(total),
-           "mem_used_gb": gb(s.native.mem_free_before - free_after) if free_after is not None else None}
+           "mem_used_gb": gb(s.native.mem_free_before - free_after) if free_after is not None else None,
+           "phases": phases}
     print(json.dumps(out), flush=True)
     return 0
 
