@@ -112,7 +112,8 @@ std::string Config::usage() {
      << "  --lag auto|on|off         lagged convergence check of overlapped sweeps (3rd field buffer)\n"
      << "  --no-block-overlap        block decompositions: exchange the halo first, then sweep\n"
      << "  --no-long-sweeps          step-count remainders as partial sweeps, not K+1-step sweeps\n"
-     << "  --no-autotune             x schedule of the sweeps from the dispatch model, not timed at start-up\n"
+     << "  --autotune auto|on|off    time the sweep schedule candidates (z stride, x segments) at start-up;\n"
+     << "                            auto: single-subdomain runs (--no-autotune = off)\n"
      << "  --graph-multistream       record the overlapped multi-stream schedule into hipGraphs too\n"
      << "  --no-rccl-graph           never record RCCL calls into hipGraphs (eager multi-rank steps)\n"
      << "  --rccl-shared             one RCCL communicator for halos and all-reduces\n"
@@ -228,7 +229,14 @@ Config Config::parse(int argc, const char* const* argv) {
     }
     else if (key == "--no-block-overlap") c.block_overlap = false;
     else if (key == "--no-long-sweeps") c.long_sweeps = false;
-    else if (key == "--no-autotune") c.autotune = false;
+    else if (key == "--no-autotune") c.autotune = 0;
+    else if (key == "--autotune") {
+      const std::string v = get("--autotune");
+      if (v == "auto") c.autotune = -1;
+      else if (v == "on") c.autotune = 1;
+      else if (v == "off") c.autotune = 0;
+      else throw UsageError("--autotune auto|on|off, not '" + v + "'");
+    }
     else if (key == "--graph-multistream") c.graph_multistream = true;
     else if (key == "--rccl-graph") c.rccl_graph = true;
     else if (key == "--no-rccl-graph") c.rccl_graph = false;

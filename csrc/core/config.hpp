@@ -74,7 +74,9 @@ struct Config {
   int lag = -1;                   // lagged convergence check of overlapped sweeps (third buffer): -1 auto, 0 off, 1 on
   bool block_overlap = true;      // block decompositions: interior || halo (false: exchange first)
   bool long_sweeps = true;        // K+1-step sweeps absorb step counts that are not multiples of K
-  bool autotune = true;           // time the interior sweeps' x-schedule candidates at initialisation
+  // time the interior sweeps' schedule candidates at initialisation: -1 auto
+  // (single-subdomain runs, whose sweeps run alone as they are timed), 0 off, 1 on
+  int autotune = -1;
   bool graph_multistream = false; // record the overlapped multi-stream schedule into hipGraphs too
   bool rccl_graph = true;         // RCCL calls may be recorded into hipGraphs (tests/test_gpu_rccl.py)
   bool rccl_shared = false;       // one RCCL communicator for halos and all-reduces (else ncclCommSplit)

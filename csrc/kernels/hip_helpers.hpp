@@ -174,18 +174,23 @@ double walk_makespan(int64_t nx, int64_t tiles, int live, int fill, int U);
 // Compute units of the current device (cached per device).
 int device_cus();
 
-// x-schedule autotuning (round 3).  The dispatch model above picks the best
-// measured segment on the 1022^3 boxes but not on every box (the 2-GPU slab
-// share's interior, 506 x 1022^2: whole tiles 772 GLUPS, 2 segments 812;
-// profiles/xplan_calibration_r03.md), so a sweep shape can be timed once:
-// tune_x_schedule launches every candidate value of spec field L (-3 = the
-// model's x plan, > 0 fixed segments of nx/k planes) twice on `s`, keeps the
-// fastest (the model's plan unless another is >= 1.5% faster) per (device,
-// kernel, nx, tiles, slots, reserved CUs) and returns it; tuned_x_lookup
-// returns a kept choice or 0.
-int tuned_x_lookup(const void* kfn, int64_t nx, int64_t tiles, int slots, int reserved);
-int tune_x_schedule(const char* name, const void* kfn, int64_t nx, int64_t tiles, int slots, int reserved, int U,
-                    hipStream_t s, const std::function<void(int)>& launch);
+// Sweep-schedule autotuning (round 3).  The dispatch model above picks the
+// best measured x segment on the 1022^3 boxes but not on every box, and the
+// z-stride rule was set by proxies (the 8-GPU slab share's interior,
+// 122 x 1022^2, runs 774 GLUPS with 56-column tiles against 723 with 58;
+// profiles/xplan_calibration_r03.md).  tune_schedule times, twice each, every
+// (z stride, spec field L) candidate on `s` — per stride in zs_opts the
+// model's x plan (L = -3) and fixed segments of nx/k planes — keeps the
+// fastest (the model's choice, candidate 0, unless another is >= 1.5% faster
+// in a confirming interleaved rerun) per (device, kernel, box, slots,
+// reserved CUs) and returns it; tuned_lookup returns a kept choice.
+struct SchedChoice {
+  int zs = 0, L = 0;
+};
+bool tuned_lookup(const void* kfn, const int64_t box[3], int slots, int reserved, SchedChoice* out);
+SchedChoice tune_schedule(const char* name, const void* kfn, const int64_t box[3], int slots, int reserved, int U,
+                          const std::vector<int>& zs_opts, hipStream_t s,
+                          const std::function<void(int, int)>& launch);
 
 }  // namespace hip
 }  // namespace heat3d

@@ -101,12 +101,13 @@ struct XPlanInfo {
 };
 XPlanInfo describe_xplan(int64_t nx, int64_t tiles, int slots, int fill, int U, int seg);
 
-// x schedules chosen by timing (StencilParams::tune): kernel, box planes,
-// tiles, the winning spec-field-L value (-3 = the model's x plan, > 0 fixed
-// segments) and the measured ms of the winner and of the model's plan
+// sweep schedules chosen by timing (StencilParams::tune): kernel, box, the
+// winning z tile stride and spec-field-L value (-3 = the model's x plan, > 0
+// fixed segments) and the measured ms of the winner and of the model's choice
 struct TunedSchedule {
   std::string kernel;
-  int64_t nx = 0, tiles = 0;
+  int64_t nx = 0, ny = 0, nz = 0;
+  int zs = 0;  // z tile stride
   int L = 0;
   double ms = 0, ms_model = 0;
   int candidates = 0;

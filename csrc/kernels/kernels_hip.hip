@@ -422,82 +422,95 @@ namespace {
 struct TuneKey {
   int dev;
   const void* kfn;
-  int64_t nx, tiles;
+  int64_t n0, n1, n2;
   int slots, reserved;
   bool operator<(const TuneKey& o) const {
-    return std::tie(dev, kfn, nx, tiles, slots, reserved) < std::tie(o.dev, o.kfn, o.nx, o.tiles, o.slots, o.reserved);
+    return std::tie(dev, kfn, n0, n1, n2, slots, reserved) <
+           std::tie(o.dev, o.kfn, o.n0, o.n1, o.n2, o.slots, o.reserved);
   }
 };
 std::mutex tune_mu;
 std::map<TuneKey, TunedSchedule> tune_cache;
 }  // namespace
 
-int tuned_x_lookup(const void* kfn, int64_t nx, int64_t tiles, int slots, int reserved) {
+bool tuned_lookup(const void* kfn, const int64_t box[3], int slots, int reserved, SchedChoice* out) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
   std::lock_guard<std::mutex> lk(tune_mu);
-  auto it = tune_cache.find(TuneKey{dev, kfn, nx, tiles, slots, reserved});
-  return it == tune_cache.end() ? 0 : it->second.L;
+  auto it = tune_cache.find(TuneKey{dev, kfn, box[0], box[1], box[2], slots, reserved});
+  if (it == tune_cache.end()) return false;
+  *out = SchedChoice{it->second.zs, it->second.L};
+  return true;
 }
 
-int tune_x_schedule(const char* name, const void* kfn, int64_t nx, int64_t tiles, int slots, int reserved, int U,
-                    hipStream_t s, const std::function<void(int)>& launch) {
+SchedChoice tune_schedule(const char* name, const void* kfn, const int64_t box[3], int slots, int reserved, int U,
+                          const std::vector<int>& zs_opts, hipStream_t s,
+                          const std::function<void(int, int)>& launch) {
   int dev = 0;
   HIPK_CHECK(hipGetDevice(&dev));
-  const TuneKey key{dev, kfn, nx, tiles, slots, reserved};
+  const TuneKey key{dev, kfn, box[0], box[1], box[2], slots, reserved};
   {
     std::unique_lock<std::mutex> lk(tune_mu);
     auto it = tune_cache.find(key);
     if (it != tune_cache.end()) {
-      const int L = it->second.L;
+      const SchedChoice c{it->second.zs, it->second.L};
       lk.unlock();
-      launch(L);
-      return L;
+      launch(c.zs, c.L);
+      return c;
     }
   }
-  // candidates: the model's plan, then segments of nx / k planes (distinct,
-  // >= one unrolled chunk, not the model's own segment)
-  std::vector<int> cand{-3};
-  for (int k : {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16}) {
-    const int seg = (int)((nx + k - 1) / k);
-    if (seg < U || seg >= (1 << 15)) continue;
-    if (std::find(cand.begin(), cand.end(), seg) != cand.end()) continue;
-    cand.push_back(seg);
+  HEAT3D_CHECK(!zs_opts.empty(), "tune_schedule: no z stride");
+  const int64_t nx = box[0];
+  // candidates: per z stride, the model's x plan and segments of nx / k
+  // planes (distinct, >= one unrolled chunk); candidate 0 = the model's
+  // stride and plan, the reference every other must beat by 1.5 %
+  std::vector<SchedChoice> cand;
+  for (int zs : zs_opts) {
+    cand.push_back({zs, -3});
+    std::vector<int> segs;
+    for (int k : {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16}) {
+      const int seg = (int)((nx + k - 1) / k);
+      if (seg < U || seg >= (1 << 15) || std::find(segs.begin(), segs.end(), seg) != segs.end()) continue;
+      segs.push_back(seg);
+      cand.push_back({zs, seg});
+    }
   }
   hipEvent_t e0, e1;
   HIPK_CHECK(hipEventCreate(&e0));
   HIPK_CHECK(hipEventCreate(&e1));
+  // a candidate's time: `reps` back-to-back sweeps between two events, per
+  // sweep (a single sub-millisecond sweep after a host wait measures launch
+  // latency and clock ramp-up, not the schedule: the 8-GPU share's interior
+  // timed 0.65 ms alone against 0.53 ms in a stream of sweeps)
+  int reps = 1;
+  auto timed = [&](const SchedChoice& c) {
+    HIPK_CHECK(hipEventRecord(e0, s));
+    for (int i = 0; i < reps; ++i) launch(c.zs, c.L);
+    HIPK_CHECK(hipEventRecord(e1, s));
+    HIPK_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPK_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    return ms / reps;
+  };
   std::vector<float> best(cand.size(), 1e30f);
-  launch(-3);  // warm: code object, caches, clocks
-  for (int rep = 0; rep < 2; ++rep) {
-    for (std::size_t i = 0; i < cand.size(); ++i) {
-      HIPK_CHECK(hipEventRecord(e0, s));
-      launch(cand[i]);
-      HIPK_CHECK(hipEventRecord(e1, s));
-      HIPK_CHECK(hipEventSynchronize(e1));
-      float ms = 0;
-      HIPK_CHECK(hipEventElapsedTime(&ms, e0, e1));
-      best[i] = std::min(best[i], ms);
-    }
-  }
+  // warm (code object, caches, clocks), then size the repetitions to >= 4 ms
+  launch(cand[0].zs, cand[0].L);
+  reps = 3;
+  const float t1 = timed(cand[0]);
+  reps = std::max(1, std::min(16, (int)std::ceil(4.0f / std::max(1e-3f, t1))));
+  for (int rep = 0; rep < 2; ++rep)
+    for (std::size_t i = 0; i < cand.size(); ++i) best[i] = std::min(best[i], timed(cand[i]));
   std::size_t w = 0;
   for (std::size_t i = 1; i < cand.size(); ++i)
     if (best[i] < best[w]) w = i;
-  if (best[w] > best[0] / 1.015f) w = 0;  // ties go to the model's plan
+  if (best[w] > best[0] / 1.015f) w = 0;  // ties go to the model's choice
   if (w != 0) {
-    // confirm against the model's plan, interleaved: a rival process on the
+    // confirm against the model's choice, interleaved: a rival process on the
     // same GPU (or a clock step) during one candidate's runs must not decide
     float bw = 1e30f, b0 = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
-      for (int j = 0; j < 2; ++j) {
-        HIPK_CHECK(hipEventRecord(e0, s));
-        launch(j ? cand[w] : cand[0]);
-        HIPK_CHECK(hipEventRecord(e1, s));
-        HIPK_CHECK(hipEventSynchronize(e1));
-        float ms = 0;
-        HIPK_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        (j ? bw : b0) = std::min(j ? bw : b0, ms);
-      }
+      b0 = std::min(b0, timed(cand[0]));
+      bw = std::min(bw, timed(cand[w]));
     }
     best[w] = std::min(best[w], bw);
     best[0] = std::min(best[0], b0);
@@ -507,20 +520,23 @@ int tune_x_schedule(const char* name, const void* kfn, int64_t nx, int64_t tiles
   (void)hipEventDestroy(e1);
   TunedSchedule t;
   t.kernel = name;
-  t.nx = nx;
-  t.tiles = tiles;
-  t.L = cand[w];
+  t.nx = box[0];
+  t.ny = box[1];
+  t.nz = box[2];
+  t.zs = cand[w].zs;
+  t.L = cand[w].L;
   t.ms = best[w];
   t.ms_model = best[0];
   t.candidates = (int)cand.size();
   if (std::getenv("HEAT3D_TRACE")) {
-    std::fprintf(stderr, "[heat3d trace] x-schedule %s nx=%lld tiles=%lld:", name, (long long)nx, (long long)tiles);
-    for (std::size_t i = 0; i < cand.size(); ++i) std::fprintf(stderr, " %d:%.3f", cand[i], best[i]);
-    std::fprintf(stderr, " -> %d\n", t.L);
+    std::fprintf(stderr, "[heat3d trace] schedule %s box %lldx%lldx%lld (%d reps):", name, (long long)box[0],
+                 (long long)box[1], (long long)box[2], reps);
+    for (std::size_t i = 0; i < cand.size(); ++i) std::fprintf(stderr, " %d/%d:%.3f", cand[i].zs, cand[i].L, best[i]);
+    std::fprintf(stderr, " -> %d/%d\n", t.zs, t.L);
   }
   std::lock_guard<std::mutex> lk(tune_mu);
   tune_cache[key] = t;
-  return t.L;
+  return cand[w];
 }
 
 std::vector<TunedSchedule> tuned_schedules() {

@@ -451,12 +451,15 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   const int ZS = ks.ZS > 0 ? ks.ZS
                            : lean_z_stride(b.extent(0), b.extent(1), b.extent(2), K, (int)sizeof(Real), TY, slots, U, ks.L);
   HEAT3D_CHECK(ZS >= 1 && ZS <= 64 - 2 * K, "tl: z stride " << ZS << " outside [1, " << 64 - 2 * K << "]");
-  g.zs = ZS;
   g.c00 = (int)(b.lo[2] - K);
   g.r00 = (int)(b.lo[1] - K);
-  g.nzb = (int)std::max<int64_t>(1, (b.extent(2) + ZS - 1) / ZS);
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
-  const int64_t ntiles = (int64_t)g.nzb * g.nyb;
+  auto set_zs = [&](TBLArgs& ga, int zs) {
+    ga.zs = zs;
+    ga.nzb = (int)std::max<int64_t>(1, (b.extent(2) + zs - 1) / zs);
+    return (int64_t)ga.nzb * ga.nyb;
+  };
+  const int64_t ntiles = set_zs(g, ZS);
   const int64_t nxb = b.extent(0);
   // workgroups the stream can hold at once (CUs kept off it by a CU mask
   // are not there for the persistent walk)
@@ -498,11 +501,12 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
     }
   }
   // spec field L: > 0 fixed segments, -1 equal segments, -2 persistent walk,
-  // -3 the x plan; 0: the schedule timed for this shape (tune_x_schedule),
-  // else the x plan
-  auto fire = [&](int Lx) {
+  // -3 the x plan; 0: the schedule timed for this box (tune_schedule: z
+  // stride and x schedule), else the x plan
+  auto fire = [&](int zs, int Lx) {
     TBLArgs ga = g;
-    const XPlan xp = Lx > 0 ? fixed_xplan(nxb, ntiles, Lx) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, Lx == -1);
+    const int64_t tiles = set_zs(ga, zs);
+    const XPlan xp = Lx > 0 ? fixed_xplan(nxb, tiles, Lx) : plan_x(nxb, tiles, slots, 2 * (K - 1), U, Lx == -1);
     HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl: x plan out of range");
     ga.segsplit = xp.seg | (xp.split << 16);
     ga.n1 = xp.n1;
@@ -510,25 +514,34 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
     const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
     HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
     if (std::getenv("HEAT3D_TRACE"))
-      std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: L=%d seg=%d tiles=%dx%d blocks=%lld (model %.1f)\n",
-                   K, (long long)nxb, Lx, xp.seg, g.nzb, g.nyb, (long long)nblocks,
-                   xplan_makespan(xp, nxb, ntiles, slots, 2 * (K - 1), U));
+      std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: zs=%d L=%d seg=%d tiles=%dx%d blocks=%lld (model %.1f)\n",
+                   K, (long long)nxb, zs, Lx, xp.seg, ga.nzb, ga.nyb, (long long)nblocks,
+                   xplan_makespan(xp, nxb, tiles, slots, 2 * (K - 1), U));
     hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, false>), dim3((unsigned)nblocks), dim3(64 * WY), 0,
                        s, static_cast<const Real*>(p.in), static_cast<Real*>(p.out), ga, (Real)p.D[0], (Real)p.D[1],
                        (Real)p.D[2], r, done);
     HIPK_CHECK(hipGetLastError());
   };
-  if (ks.L == 0 && !SW) {
+  if (ks.L == 0 && ks.ZS == 0 && !SW) {
+    const int64_t box[3] = {b.extent(0), b.extent(1), b.extent(2)};
     if (p.tune) {
-      tune_x_schedule(SW ? "tl-y" : sizeof(Real) == 8 ? "tl-fp64" : "tl-fp32", kfn, nxb, ntiles, slots,
-                      p.cu_reserved, U, s, fire);
+      // z strides: the model's, and the other of 64 - 2K / its 64-byte-aligned form
+      std::vector<int> zs_opts{ZS};
+      const int wide = 64 - 2 * K, aligned = sizeof(Real) == 8 ? wide & ~7 : wide;
+      for (int z : {wide, aligned})
+        if (std::find(zs_opts.begin(), zs_opts.end(), z) == zs_opts.end()) zs_opts.push_back(z);
+      tune_schedule(sizeof(Real) == 8 ? "tl-fp64" : "tl-fp32", kfn, box, slots, p.cu_reserved, U, zs_opts, s, fire);
       return;  // every candidate computed this sweep
     }
-    const int t = tuned_x_lookup(kfn, nxb, ntiles, slots, p.cu_reserved);
-    fire(t != 0 ? t : 0);
+    SchedChoice c;
+    if (tuned_lookup(kfn, box, slots, p.cu_reserved, &c)) {
+      fire(c.zs, c.L);
+      return;
+    }
+    fire(ZS, 0);
     return;
   }
-  fire(ks.L);
+  fire(ZS, ks.L);
 }
 
 // p == nullptr: only report whether the variant k resolves to exists

@@ -376,12 +376,15 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   const int ZS = ks.ZS > 0 ? ks.ZS : pair_z_stride(b.extent(0), b.extent(1), b.extent(2), K, TY, slots, U, ks.L);
   HEAT3D_CHECK(ZS >= 2 && ZS % 2 == 0 && ZS <= 128 - 2 * K - 2,
                "tl pair: z stride " << ZS << " must be even and in [2, " << 128 - 2 * K - 2 << "]");
-  g.zs = ZS;
   constexpr int YS = TY - 2 * K;
   g.r00 = (int)(b.lo[1] - K);
-  g.nzb = (int)std::max<int64_t>(1, (b.extent(2) + ZS - 1) / ZS);
   g.nyb = (int)std::max<int64_t>(1, (b.extent(1) + YS - 1) / YS);
-  const int64_t ntiles = (int64_t)g.nzb * g.nyb;
+  auto set_zs = [&](TBPArgs& ga, int zs) {
+    ga.zs = zs;
+    ga.nzb = (int)std::max<int64_t>(1, (b.extent(2) + zs - 1) / zs);
+    return (int64_t)ga.nzb * ga.nyb;
+  };
+  set_zs(g, ZS);
   const int64_t nxb = b.extent(0);
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl pair: residual slots " << p.slot << "+" << K);
   static const int spill = [] {
@@ -393,10 +396,11 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(spill == 0, "tl pair variant " << ks.str() << " spills " << spill << " B of registers per lane");
   unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
-  // spec field L as in launch_tbl (0: the timed schedule of this shape, else the x plan)
-  auto fire = [&](int Lx) {
+  // spec fields L and ZS as in launch_tbl (L = 0, ZS = 0: the timed schedule of this box)
+  auto fire = [&](int zs, int Lx) {
     TBPArgs ga = g;
-    const XPlan xp = Lx > 0 ? fixed_xplan(nxb, ntiles, Lx) : plan_x(nxb, ntiles, slots, 2 * (K - 1), U, Lx == -1);
+    const int64_t tiles = set_zs(ga, zs);
+    const XPlan xp = Lx > 0 ? fixed_xplan(nxb, tiles, Lx) : plan_x(nxb, tiles, slots, 2 * (K - 1), U, Lx == -1);
     HEAT3D_CHECK(xp.seg < (1 << 15) && xp.split < (1 << 15) && xp.r < (1 << 30), "tl pair: x plan out of range");
     ga.segsplit = xp.seg | (xp.split << 16);
     ga.n1 = xp.n1;
@@ -409,16 +413,25 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
     HIPK_CHECK(hipGetLastError());
   };
   const void* kfn = reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q, AUX>);
-  if (ks.L == 0) {
+  if (ks.L == 0 && ks.ZS == 0) {
+    const int64_t box[3] = {b.extent(0), b.extent(1), b.extent(2)};
     if (p.tune) {
-      tune_x_schedule("tl-fp32-pair", kfn, nxb, ntiles, slots, p.cu_reserved, U, s, fire);
+      std::vector<int> zs_opts{ZS};
+      const int wide = 128 - 2 * K - 2, aligned = wide & ~15;
+      for (int z : {wide, aligned})
+        if (z > 0 && std::find(zs_opts.begin(), zs_opts.end(), z) == zs_opts.end()) zs_opts.push_back(z);
+      tune_schedule("tl-fp32-pair", kfn, box, slots, p.cu_reserved, U, zs_opts, s, fire);
       return;
     }
-    const int t = tuned_x_lookup(kfn, nxb, ntiles, slots, p.cu_reserved);
-    fire(t != 0 ? t : 0);
+    SchedChoice c;
+    if (tuned_lookup(kfn, box, slots, p.cu_reserved, &c)) {
+      fire(c.zs, c.L);
+      return;
+    }
+    fire(ZS, 0);
     return;
   }
-  fire(ks.L);
+  fire(ZS, ks.L);
 }
 
 // p == nullptr: only report whether the variant k resolves to exists

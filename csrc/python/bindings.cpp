@@ -193,7 +193,9 @@ PYBIND11_MODULE(_heat3d, m) {
       py::dict d;
       d["kernel"] = t.kernel;
       d["nx"] = t.nx;
-      d["tiles"] = t.tiles;
+      d["ny"] = t.ny;
+      d["nz"] = t.nz;
+      d["zs"] = t.zs;
       d["L"] = t.L;
       d["ms"] = t.ms;
       d["ms_model"] = t.ms_model;

@@ -481,7 +481,14 @@ void Solver::initialize() {
 // overwrites with the same values.  The chosen schedules then serve every
 // eager launch and every graph capture of the run.
 void Solver::tune_schedules() {
-  if (!cfg_.autotune || !tb_ || !be_->is_gpu()) return;
+  // auto: only where a sweep runs alone as it is timed here.  Under the
+  // overlapped multi-rank schedule the interior shares the GPU with the halo
+  // chain, and a standalone timing did not predict it: the phantom 8-GPU
+  // share's interior timed 56-column / 61-plane pieces 12% faster alone, then
+  // ran 9% slower than the model's choice in the schedule (same ms per step;
+  // profiles/rank_proxy_r03.md)
+  const bool on = cfg_.autotune > 0 || (cfg_.autotune < 0 && !has_halo_ && local_.size() == 1);
+  if (!on || !tb_ || !be_->is_gpu()) return;
   std::vector<KernelSpec> specs{kspec2_};
   if (!has_halo_ && cfg_.long_sweeps && K_ + 1 <= 6 && K_ + 1 <= kResidualSlots) {
     KernelSpec ks;

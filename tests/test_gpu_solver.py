@@ -167,7 +167,8 @@ def test_schedule_autotune_bitwise(h3d, gpu, vr):
     the run with the dispatch model's schedule (--no-autotune)."""
     n, iters = (200, 67, 131), 61
     kw = dict(virtual_ranks=vr, decomp=(vr, 1, 1)) if vr > 1 else {}
-    a = h3d.HeatSolver(n, iters, 0.0, backend="hip", **kw)
+    # auto tunes single-subdomain runs only; "on" forces it for the slabs too
+    a = h3d.HeatSolver(n, iters, 0.0, backend="hip", extra_args=["--autotune", "on" if vr > 1 else "auto"], **kw)
     b = h3d.HeatSolver(n, iters, 0.0, backend="hip", extra_args=["--no-autotune"], **kw)
     ra, rb = a.run(), b.run()
     assert ra["iterations"] == rb["iterations"] == iters and ra["last_residual"] == rb["last_residual"]

@@ -37,8 +37,11 @@ def main() -> int:
     ap.add_argument("--ar-us", type=float, default=20.0, help="emulated all-reduce latency (us)")
     ap.add_argument("--backend", default="hip")
     ap.add_argument("--extra", default="", help="extra solver flags, e.g. '--no-overlap'")
+    ap.add_argument("--trace-schedule", action="store_true",
+                    help="print the start-up schedule tuner's candidate timings (HEAT3D_TRACE during initialize)")
     args = ap.parse_args()
 
+    import heat3d_amd
     from heat3d_amd import HeatSolver
     from heat3d_amd.parallel import best_dims_for
 
@@ -54,7 +57,10 @@ def main() -> int:
                    device=0 if args.backend == "hip" else None, phantom=(r, P),
                    extra_args=["--phantom-gbps", str(args.gbps), "--phantom-allreduce-us", str(args.ar_us)]
                    + (args.extra.split() if args.extra else []))
+    if args.trace_schedule:
+        os.environ["HEAT3D_TRACE"] = "1"
     s.initialize()
+    os.environ.pop("HEAT3D_TRACE", None)
     free_after, total = s.native.mem_info()
     s.step(args.warmup)
     s.synchronize()
@@ -78,7 +84,9 @@ def main() -> int:
            "mem_planned_gb": gb(s.native.planned_bytes), "mem_free_before_gb": gb(s.native.mem_free_before),
            "mem_free_after_gb": gb(free_after), "mem_total_gb": gb(total),
            "mem_used_gb": gb(s.native.mem_free_before - free_after) if free_after is not None else None,
-           "phases": phases}
+           "phases": phases,
+           "x_schedules": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in t.items()}
+                           for t in heat3d_amd.native().tuned_schedules()]}
     print(json.dumps(out), flush=True)
     return 0
 
