@@ -170,6 +170,11 @@ def run_rank(args) -> int:
     # all-reduce traffic goes through the native RCCL communicator
     info, group = init_process_group("gloo" if world > 1 else None)
     rank = info.rank
+    if args.rccl_host_split and world > 1 and "NCCL_HOSTID" not in os.environ:
+        # under an external launcher (torchrun): every rank its own RCCL "host"
+        # before the communicator exists (RCCL reads these at initialisation)
+        os.environ["NCCL_HOSTID"] = f"heat3d-bench-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     ndev = ext.device_count()
     if ndev < 1:
         print("bench.py: no HIP device visible", file=sys.stderr)

@@ -85,6 +85,28 @@ def test_bench_self_launch_rccl(gpu, tmp_path):
         assert 0.0 <= q["chain_overlap_fraction"] <= 1.0 and q["sweep_ms"] >= q["interior_ms"] * 0.5, q
 
 
+def test_bench_under_torchrun_rccl(gpu, tmp_path):
+    """The driver's N-GPU launch line, ``python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P
+    bench.py --gpus 2 ...``: ranks from torchrun's environment, the gloo
+    bootstrap, real RCCL (each rank its own NCCL_HOSTID, set by bench.py
+    itself under --rccl-host-split), one JSON line from rank 0."""
+    out = tmp_path / "t.json"
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "rccl", "--rccl-host-split",
+                        "--grid", "96", "--steps", "6", "--warmup", "3", "--converge-eps", "0",
+                        "--json-out", str(out)],
+                       capture_output=True, text=True, timeout=150, cwd=ROOT,
+                       env={k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")})
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["comm_ranks"] == 2 and j["config"]["comm"] == "rccl" and j["halo_verified"]
+    assert [q["rank"] for q in j["phases"]] == [0, 1] and j == json.loads(out.read_text())
+
+
 def test_bench_self_launch_socket(gpu, tmp_path):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "socket",
                         "--grid", "128", "--steps", "6", "--warmup", "3", "--converge-eps", "0",
