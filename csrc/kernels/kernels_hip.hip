@@ -475,13 +475,15 @@ SchedChoice tune_schedule(const char* name, const void* kfn, const int64_t box[3
       cand.push_back({zs, seg});
     }
   }
-  hipEvent_t e0, e1;
-  HIPK_CHECK(hipEventCreate(&e0));
-  HIPK_CHECK(hipEventCreate(&e1));
+  struct Ev {  // released on every exit, a throwing launch included
+    hipEvent_t e = nullptr;
+    Ev() { HIPK_CHECK(hipEventCreate(&e)); }
+    ~Ev() { (void)hipEventDestroy(e); }
+  } ev0, ev1;
+  hipEvent_t e0 = ev0.e, e1 = ev1.e;
   // a candidate's time: `reps` back-to-back sweeps between two events, per
-  // sweep (a single sub-millisecond sweep after a host wait measures launch
-  // latency and clock ramp-up, not the schedule: the 8-GPU share's interior
-  // timed 0.65 ms alone against 0.53 ms in a stream of sweeps)
+  // sweep, >= 4 ms in all (short sweeps timed one at a time are dominated by
+  // launch gaps and timer noise)
   int reps = 1;
   auto timed = [&](const SchedChoice& c) {
     HIPK_CHECK(hipEventRecord(e0, s));
@@ -516,8 +518,6 @@ SchedChoice tune_schedule(const char* name, const void* kfn, const int64_t box[3
     best[0] = std::min(best[0], b0);
     if (bw > b0 / 1.015f) w = 0;
   }
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   TunedSchedule t;
   t.kernel = name;
   t.nx = box[0];
