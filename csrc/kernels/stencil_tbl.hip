@@ -584,7 +584,7 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
   // the default shapes carry the persistent-walk form
   H3D_TBLA(3, 16, 3, 2, true) H3D_TBLA(3, 16, 3, 3, false) H3D_TBLA(3, 16, 3, 17, false)
   H3D_TBLA(3, 16, 3, 18, false) H3D_TBLA(3, 16, 3, 19, false)
-  H3D_TBLA(2, 16, 4, 2, false)
+  H3D_TBLA(2, 16, 4, 2, false) H3D_TBLA(3, 16, 2, 2, false)
   H3D_TBLA(3, 12, 4, 2, true)  // the fp64 K = 4 default (long sweeps: 12 waves, 36 rows)
   H3D_TBLA(4, 12, 4, 2, false)
 #undef H3D_TBLA

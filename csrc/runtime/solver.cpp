@@ -128,14 +128,17 @@ KernelSpec KernelSpec::resolved(DType t) const {
       // input halo lines resident).  MI355X, 1024^3 kernel level: 756 -> 798
       // GLUPS, 512^3 / 768^3 +2-2.5%
       // (also K = 4, the long sweeps of step counts that are not multiples of
-      // 3: 5.45 -> 5.38 ms per 1024^3 sweep.  Not K = 2: its partial sweep went
-      // from 3.96 to 5.45 ms with nt stores; profiles/bench_r02_driver_gap.md)
+      // 3: 5.45 -> 5.38 ms per 1024^3 sweep; and K = 2, the partial sweeps of
+      // multi-rank remainders: 1022^3 557 -> 615 GLUPS, the 8-GPU slab
+      // share's interior 512 -> 526, round 3 — round 2 had measured K = 2
+      // slower with nt, profiles/bench_r02_driver_gap.md, which the round-3
+      // kernel does not reproduce: profiles/probes_r03.md)
       // fp32 packed-pair default shape too: 1388 -> 1431 GLUPS at 1024^3, 1354
       // -> 1513 at 2049^3
       if (!f64 && r.O < 0 && r.V == 2 && K == 3 && r.R == 3 && r.WY == 16 && r.NT == 3) r.O = 2;
       if (f64 && r.O < 0 && r.V == 1 && r.NT == 3 &&
           ((K == 3 && r.R == 3 && r.WY == 16) || (K == 4 && r.R == 2 && r.WY == 16) ||
-           (K == 4 && r.R == 3 && r.WY == 12)))
+           (K == 4 && r.R == 3 && r.WY == 12) || (K == 2 && r.R == 3 && r.WY == 16)))
         r.O = 2;
       break;
     default:

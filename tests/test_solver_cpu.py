@@ -274,7 +274,9 @@ def test_memory_preflight(h3d):
     assert p.native.planned_bytes > p.native.field_buffers * 24 ** 3 * 8
     with pytest.raises(Exception, match="memory preflight.*needs"):
         h3d.HeatSolver((6000, 6000, 6000), 5, 0.0, backend="cpu")
-    reserve = ["--mem-reserve-gb", str(n.mem_free_before / 1e9)]
+    # a reserve of all the memory there is (free memory moves while other
+    # test processes run: the free figure of an earlier solver is not a bound)
+    reserve = ["--mem-reserve-gb", str(n.mem_total / 1e9)]
     with pytest.raises(Exception, match="memory preflight"):
         h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu", extra_args=reserve)
     h3d.HeatSolver((40, 40, 40), 5, 0.0, backend="cpu", extra_args=reserve + ["--no-mem-preflight"])
