@@ -150,15 +150,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
   const bool zfast = c0 >= g.uzlo && c0 + 128 <= g.uzhi;
   const bool wrows = wave * R >= K && wave * R + R <= TY - K && yb >= g.uylo && yb + R <= g.uyhi &&
                      yb >= g.blo[1] && yb + R <= g.bhi[1];
-  // the mask-free step also takes every stored column in whole pairs (tiles
-  // start on even columns; the stored range starts at an even hl and ends at
-  // the tile's even stride, or at the box end an even number of columns
-  // after the tile start): one masked 8-byte store per row, no per-lane
-  // branch between pair and single stores (an odd box end, 2047^3, leaves
-  // only its last tile column to the masked step)
-  const bool pair_uniform =
-      (g.hl & 1) == 0 && (c0 + g.hl + g.zs <= g.bhi[2] || ((g.bhi[2] - c0) & 1) == 0);
-  const bool wfast = zfast && wrows && pair_uniform;
+  const bool wfast = zfast && wrows;
   const int xf_lo = max(max(x0 + 2 * (K - 1), g.ulo + K - 1), g.blo[0] + K - 1);
   const int xf_hi = min(min(xlast, g.uhi - 1), g.bhi[0] + K - 2);
 
@@ -271,18 +263,13 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
           if (cnt) m[s] = __builtin_elementwise_max(m[s], d);
         }
         if (s == K - 1 && st) {
+          nan_seen |= (zst0 && nv.x != nv.x) || (zst1 && nv.y != nv.y);
           const __amdgpu_buffer_rsrc_t ro = prs(outw + (int64_t)p * sx);
-          if constexpr (FAST) {
-            nan_seen |= zst2 && (nv.x != nv.x || nv.y != nv.y);
-            if (zst2) st2<AUX>(nv, ro, lane_b, r * sy_b);
+          if (zst2) {
+            st2<AUX>(nv, ro, lane_b, r * sy_b);
           } else {
-            nan_seen |= (zst0 && nv.x != nv.x) || (zst1 && nv.y != nv.y);
-            if (zst2) {
-              st2<AUX>(nv, ro, lane_b, r * sy_b);
-            } else {
-              if (zst0) st1<AUX>(nv.x, ro, lane_b, r * sy_b);
-              if (zst1) st1<AUX>(nv.y, ro, lane_b + 4u, r * sy_b);
-            }
+            if (zst0) st1<AUX>(nv.x, ro, lane_b, r * sy_b);
+            if (zst1) st1<AUX>(nv.y, ro, lane_b + 4u, r * sy_b);
           }
         }
       }
