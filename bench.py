@@ -81,6 +81,11 @@ def parse_args(argv=None):
                          "events at the schedule's phase boundaries (JSON 'phases'; 0 disables)")
     ap.add_argument("--watchdog", type=float, default=300.0,
                     help="native watchdog (s): a rank whose peers stop making progress aborts its communicators")
+    ap.add_argument("--preheat-ms", type=float, default=20.0,
+                    help="untimed GPU warm-up right before the timed window: repetitions of the next sweep's "
+                         "interior into the buffer it will overwrite, without residual state (the solver state "
+                         "is untouched), so the timed steps do not start on a GPU idled by the graph capture "
+                         "(0 disables)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -233,6 +238,16 @@ def run_rank(args) -> int:
     phase("halos verified")
     warm = s.native.iterations_issued
     g0 = s.native.graph_launches
+    # The graph capture above (12 ms for the 1024^3 timed graph) outlasts a
+    # short warm-up on the GPU, which then idles and clocks down: the first
+    # timed sweeps of the driver's 20-step run ran 7-12% slow (kernel trace,
+    # profiles/bench_r03_preheat.md).  Keep the GPU at work until the timed
+    # window with sweeps that leave the solver state as it is.
+    K = s.native.temporal_steps
+    est_ms = s.interior_points / world * max(1, K) / ((800e9 if args.dtype == "fp64" else 1400e9)) * 1e3
+    preheat = (s.native.preheat(max(1, min(64, int(args.preheat_ms / max(est_ms, 1e-3)) + 1)))
+               if args.preheat_ms > 0 else 0)
+    phase("preheat enqueued")
     barrier(group)
     torch.cuda.synchronize()
     phase("barrier")
@@ -254,7 +269,6 @@ def run_rank(args) -> int:
     kernel = s.kernel
     comm_name = s.native.comm_name
     comm_ranks = s.native.comm_transport_ranks
-    K = s.native.temporal_steps
     nbuf = s.native.field_buffers
     reserved = s.native.reserved_cus
     # the x schedules timed at start-up (Config autotune): L = -3 is the
@@ -309,7 +323,8 @@ def run_rank(args) -> int:
                    "kernel": kernel, "temporal_K": K, "field_buffers": nbuf,
                    "graph_requested": not args.no_graph, "graph_used": graph_launches > 0,
                    "graph_launches": graph_launches,
-                   "overlap": not args.no_overlap, "comm": comm_name, "reserved_cus": reserved},
+                   "overlap": not args.no_overlap, "comm": comm_name, "reserved_cus": reserved,
+                   "preheat_sweeps": preheat},
         "comm_ranks": comm_ranks,
         "placement": placement,
         "halo_verified": True,

@@ -620,6 +620,10 @@ PYBIND11_MODULE(_heat3d, m) {
         py::gil_scoped_release nogil;
         s.prepare_steps(n);
       })
+      .def("preheat", [](Solver& s, int sweeps) {
+        py::gil_scoped_release nogil;
+        return s.preheat(sweeps);
+      })
       .def("state", [](Solver& s) {
         HostState h = s.state();
         py::dict d;

@@ -128,17 +128,17 @@ KernelSpec KernelSpec::resolved(DType t) const {
       // input halo lines resident).  MI355X, 1024^3 kernel level: 756 -> 798
       // GLUPS, 512^3 / 768^3 +2-2.5%
       // (also K = 4, the long sweeps of step counts that are not multiples of
-      // 3: 5.45 -> 5.38 ms per 1024^3 sweep; and K = 2, the partial sweeps of
-      // multi-rank remainders: 1022^3 557 -> 615 GLUPS, the 8-GPU slab
-      // share's interior 512 -> 526, round 3 — round 2 had measured K = 2
-      // slower with nt, profiles/bench_r02_driver_gap.md, which the round-3
-      // kernel does not reproduce: profiles/probes_r03.md)
+      // 3: 5.45 -> 5.38 ms per 1024^3 sweep.  Not K = 2, the partial sweeps
+      // of multi-rank remainders: alone, back to back, nt is faster (1022^3
+      // 557 -> 615 GLUPS), but after a K = 3 sweep, where the solver runs it,
+      // it takes 5.26-5.45 ms against 3.96 without nt; profiles/probes_r03.md,
+      // bench_r02_driver_gap.md)
       // fp32 packed-pair default shape too: 1388 -> 1431 GLUPS at 1024^3, 1354
       // -> 1513 at 2049^3
       if (!f64 && r.O < 0 && r.V == 2 && K == 3 && r.R == 3 && r.WY == 16 && r.NT == 3) r.O = 2;
       if (f64 && r.O < 0 && r.V == 1 && r.NT == 3 &&
           ((K == 3 && r.R == 3 && r.WY == 16) || (K == 4 && r.R == 2 && r.WY == 16) ||
-           (K == 4 && r.R == 3 && r.WY == 12) || (K == 2 && r.R == 3 && r.WY == 16)))
+           (K == 4 && r.R == 3 && r.WY == 12)))
         r.O = 2;
       break;
     default:
@@ -523,6 +523,38 @@ void Solver::tune_schedules() {
     }
   }
   be_->sync(kCompute);
+}
+
+int Solver::preheat(int sweeps) {
+  if (!tb_ || !be_->is_gpu() || sweeps <= 0) return 0;
+  join_pipeline();
+  const int Kp = K_;
+  int n = 0;
+  for (int i = 0; i < sweeps; ++i) {
+    for (auto& l : local_) {
+      if (l.tb_interior.empty()) continue;
+      StencilParams sp;
+      sp.in = l.field[cur()];
+      sp.out = l.field[nxt(cur())];
+      sp.L = l.L;
+      sp.box = l.tb_interior;
+      for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+      sp.state = nullptr;
+      sp.cu_reserved = be_->reserved_cus();
+      auto shrink = [&](const int64_t (&u)[2], int64_t nn, int64_t (&o)[2]) {
+        o[0] = u[0] < 0 ? -(Kp - 1) : u[0];
+        o[1] = u[1] > nn ? nn + Kp - 1 : u[1];
+      };
+      shrink(l.ux, l.sd.n[0], sp.ux);
+      shrink(l.uy, l.sd.n[1], sp.uy);
+      shrink(l.uz, l.sd.n[2], sp.uz);
+      be_->sweep(dt_, sp, kspec2_, kCompute);
+      ++n;
+    }
+  }
+  // the next sweep's inputs and events are as they were: later work orders
+  // behind the preheat through the compute stream
+  return n;
 }
 
 // --- one iteration -----------------------------------------------------------

@@ -88,6 +88,11 @@ class Solver {
   void initialize();
   // x-schedule autotuning of the interior sweeps (Config::autotune)
   void tune_schedules();
+  // Untimed GPU warm-up that leaves the solver state untouched: `sweeps`
+  // repetitions of the next sweep's interior, written into the buffer that
+  // sweep will overwrite, without residual state (a sweep is idempotent).
+  // Asynchronous on the compute stream; returns the sweeps issued.
+  int preheat(int sweeps);
   // Full solve: iterate until converged or iter_max (heat3D.cu:541-1073).
   RunResult run();
   // Enqueue exactly n iterations without host polling (benchmarks); async.
