@@ -130,9 +130,8 @@ KernelSpec KernelSpec::resolved(DType t) const {
       // (also K = 4, the long sweeps of step counts that are not multiples of
       // 3: 5.45 -> 5.38 ms per 1024^3 sweep.  Not K = 2, the partial sweeps
       // of multi-rank remainders: alone, back to back, nt is faster (1022^3
-      // 557 -> 615 GLUPS), but after a K = 3 sweep, where the solver runs it,
-      // it takes 5.26-5.45 ms against 3.96 without nt; profiles/probes_r03.md,
-      // bench_r02_driver_gap.md)
+      // 557 -> 615 GLUPS), but where the solver runs it both policies take
+      // 5.3-5.6 ms; profiles/probes_r03.md)
       // fp32 packed-pair default shape too: 1388 -> 1431 GLUPS at 1024^3, 1354
       // -> 1513 at 2049^3
       if (!f64 && r.O < 0 && r.V == 2 && K == 3 && r.R == 3 && r.WY == 16 && r.NT == 3) r.O = 2;
