@@ -143,3 +143,16 @@ def test_threads_per_rank_cli(heat3d_bin, tmp_path, gpus, decomp, temporal):
 def test_threads_per_rank_needs_devices(heat3d_bin, tmp_path):
     r = run_cli(["23", "23", "23", "10", "1e-4", "--backend", "hip", "--gpus", "64"], tmp_path)
     assert r.returncode != 0
+
+
+def test_schedule_flags(heat3d_bin, tmp_path):
+    """--autotune auto|on|off and --no-autotune parse (round 3); a bad value
+    is a usage error with a non-zero exit; --help lists the flag."""
+    ok = run_cli(["27", "27", "27", "50", "0", "--backend", "cpu", "--autotune", "on", "--output", "none"], tmp_path)
+    assert ok.returncode == 0, ok.stdout + ok.stderr
+    ok = run_cli(["27", "27", "27", "50", "0", "--backend", "cpu", "--no-autotune", "--output", "none"], tmp_path)
+    assert ok.returncode == 0, ok.stdout + ok.stderr
+    bad = run_cli(["27", "27", "27", "50", "0", "--backend", "cpu", "--autotune", "sometimes"], tmp_path)
+    assert bad.returncode != 0 and "--autotune auto|on|off" in (bad.stdout + bad.stderr)
+    h = run_cli(["--help"], tmp_path)
+    assert "--autotune auto|on|off" in h.stdout + h.stderr
