@@ -86,6 +86,11 @@ def parse_args(argv=None):
                          "interior into the buffer it will overwrite, without residual state (the solver state "
                          "is untouched), so the timed steps do not start on a GPU idled by the graph capture "
                          "(0 disables)")
+    ap.add_argument("--progress", type=float, default=30.0,
+                    help="time-to-converge run: stderr heartbeat (iteration, relative residual, GLUPS) every S "
+                         "seconds (0 disables)")
+    ap.add_argument("--verbose", type=int, default=0,
+                    help="time-to-converge run: print the residual every N iterations (stdout, rank 0)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -201,13 +206,13 @@ def run_rank(args) -> int:
         N = tuple(d * args.weak_block + 2 for d in dims)
         G = N[0]
 
-    def make(eps, iter_max):
+    def make(eps, iter_max, extra=()):
         return HeatSolver(N, iter_max=iter_max, eps=eps, dtype=args.dtype, backend="hip",
                           decomp=dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
                           device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
                           extra_args=["--temporal", str(args.temporal), "--kernel2", args.kernel2,
-                                      "--watchdog", str(args.watchdog)])
+                                      "--watchdog", str(args.watchdog)] + list(extra))
 
     phase_log = os.environ.get("HEAT3D_BENCH_PHASES") == "1"
     tp = [time.perf_counter()]
@@ -289,7 +294,8 @@ def run_rank(args) -> int:
 
     ttc = None
     if args.converge_eps and args.converge_eps > 0:
-        c = make(args.converge_eps, 10 ** 7)
+        c = make(args.converge_eps, 10 ** 7,
+                 ["--progress", str(args.progress)] + (["--verbose", str(args.verbose)] if args.verbose > 0 else []))
         c.initialize()
         barrier(group)
         r = c.run()

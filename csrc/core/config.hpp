@@ -66,6 +66,7 @@ struct Config {
   std::string restart;
   std::string json_out;
   int verbose = 0;
+  double progress_s = 0;          // run(): stderr heartbeat period (0 = off)
   bool quiet = false;
   int cpu_threads = 0;
   int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules

@@ -162,6 +162,8 @@ struct XPlan {
 // Chosen by simulating greedy in-order dispatch onto `slots` resident
 // workgroups (cost of a piece: its planes + `fill` pipeline planes, rounded up
 // to chunks of U); cached per shape.  equal_only: no split (previous policy).
+// HEAT3D_TRACE launch diagnostics (read once per process)
+bool trace_enabled();
 XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_only = false);
 XPlan fixed_xplan(int64_t nx, int64_t tiles, int seg);
 // Makespan of a plan in the same greedy-dispatch model (plane steps per slot).

@@ -64,6 +64,9 @@ struct StencilParams {
   // idempotent: every candidate writes the same T^{n+K} to out) and keep the
   // fastest for this kernel and box shape (autotune_x_schedule)
   bool tune = false;
+  // false: the kernel honours state->done (a no-op once converged) but
+  // records no residual (Solver::preheat's idempotent warm-up sweeps)
+  bool residual = true;
 };
 
 struct InitParams {

@@ -85,7 +85,7 @@ static void stencil_t(const StencilParams& p) {
       std::memcpy(&bits, &lres, sizeof(bits));
       resbits = bits > resbits ? bits : resbits;
     }
-  if (p.state) {
+  if (p.state && p.residual) {
     unsigned long long* slot = &p.state->residual[p.slot];
     if (resbits > *slot) *slot = resbits;
   }

@@ -236,6 +236,14 @@ __global__ __launch_bounds__(64 * WZ * WY) void stencil_tile(const Real* __restr
 // large static LDS (it returned 8 x 1024-thread groups per CU for the 98 KiB
 // tr3 kernel, which fits once in the 160 KiB of a CU), so the result is capped
 // by our own LDS / wave-slot / VGPR bound.  HEAT3D_TRACE=1 prints both.
+bool trace_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT3D_TRACE");
+    return e && *e && e[0] != '0';
+  }();
+  return on;
+}
+
 int device_cus() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -272,7 +280,7 @@ int device_slots(const void* kernel, int block) {
     own = std::min(own, (4 * per_simd) / std::max(1, waves));
   }
   const int pick = std::max(1, std::min(per, own));
-  if (std::getenv("HEAT3D_TRACE"))
+  if (trace_enabled())
     std::fprintf(stderr, "[heat3d trace] device_slots: cus=%d api=%d own=%d lds=%zu vgpr=%d -> %d/CU\n", cus, per,
                  own, (size_t)a.sharedSizeBytes, a.numRegs, pick);
   return std::max(1, cus * pick);
@@ -528,7 +536,7 @@ SchedChoice tune_schedule(const char* name, const void* kfn, const int64_t box[3
   t.ms = best[w];
   t.ms_model = best[0];
   t.candidates = (int)cand.size();
-  if (std::getenv("HEAT3D_TRACE")) {
+  if (trace_enabled()) {
     std::fprintf(stderr, "[heat3d trace] schedule %s box %lldx%lldx%lld (%d reps):", name, (long long)box[0],
                  (long long)box[1], (long long)box[2], reps);
     for (std::size_t i = 0; i < cand.size(); ++i) std::fprintf(stderr, " %d/%d:%.3f", cand[i].zs, cand[i].L, best[i]);
@@ -582,7 +590,7 @@ static void launch_tile(const StencilParams& p, const KernelSpec& k, hipStream_t
   HEAT3D_CHECK(g.nblocks < (1LL << 31), "too many blocks");
   g.xq = (int)(g.nblocks / 8);
   g.xr = (int)(g.nblocks % 8);
-  unsigned long long* res = p.state ? &p.state->residual[p.slot] : nullptr;
+  unsigned long long* res = p.state && p.residual ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
   hipLaunchKernelGGL((stencil_tile<Real, V, R, WZ, WY>), dim3((unsigned)g.nblocks),
                      dim3(64 * WZ * WY), 0, s, static_cast<const Real*>(p.in),
@@ -600,7 +608,7 @@ static void launch_naive(const StencilParams& p, hipStream_t s) {
   const Box& b = p.box;
   dim3 grid((unsigned)((b.extent(2) + 63) / 64), (unsigned)((b.extent(1) + 3) / 4),
             (unsigned)((b.extent(0) + 63) / 64));
-  unsigned long long* res = p.state ? &p.state->residual[p.slot] : nullptr;
+  unsigned long long* res = p.state && p.residual ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
   hipLaunchKernelGGL(stencil_naive<Real>, grid, dim3(256), 0, s, static_cast<const Real*>(p.in),
                      static_cast<Real*>(p.out), p.L, b, (Real)p.D[0], (Real)p.D[1], (Real)p.D[2],

@@ -35,7 +35,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <type_traits>
 
@@ -377,7 +380,24 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
 // boxes of >= 500 x planes: the slab shares of the 4- and 8-GPU runs (250 and
 // 122 interior planes) lost 13% and 8% with it in the phantom-rank proxy
 // while the 2-GPU share (510 planes) gained 1.5%.
+static int lean_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U, int L);
 int lean_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U, int L) {
+  // memoised: every eager launch asks (the N > 1 schedule is eager)
+  static std::mutex mu;
+  static std::map<std::array<int64_t, 9>, int> memo;
+  const std::array<int64_t, 9> key{nx, ny, nz, K, esize, TY, slots, U, L};
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+  }
+  const int zs = lean_z_stride_plan(nx, ny, nz, K, esize, TY, slots, U, L);
+  std::lock_guard<std::mutex> lk(mu);
+  memo[key] = zs;
+  return zs;
+}
+
+static int lean_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int esize, int TY, int slots, int U, int L) {
   const int wide = 64 - 2 * K;
   const int aligned = esize == 8 ? wide & ~7 : wide;
   if (aligned == wide || aligned <= 0 || nx < 500) return wide;
@@ -481,7 +501,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
   static const int spill = scratch(kfn);
   // a spilling variant is refused (one was miscompiled on ROCm 7.2)
   HEAT3D_CHECK(spill == 0, "tl variant " << ks.str() << " spills " << spill << " B of registers per lane");
-  unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
+  unsigned long long* r = p.state && p.residual ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
   if constexpr (WALK) {
     if (walk) {
@@ -490,7 +510,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
       g.rb = -1;
       static const int spill_w = scratch(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>));
       HEAT3D_CHECK(spill_w == 0, "tl walk variant " << ks.str() << " spills " << spill_w << " B per lane");
-      if (std::getenv("HEAT3D_TRACE"))
+      if (trace_enabled())
         std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: walk tiles=%dx%d blocks=%d\n", K, (long long)nxb,
                      g.nzb, g.nyb, g.n1);
       hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>), dim3((unsigned)g.n1), dim3(64 * WY), 0, s,
@@ -513,7 +533,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
     ga.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
     const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
     HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
-    if (std::getenv("HEAT3D_TRACE"))
+    if (trace_enabled())
       std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: zs=%d L=%d seg=%d tiles=%dx%d blocks=%lld (model %.1f)\n",
                    K, (long long)nxb, zs, Lx, xp.seg, ga.nzb, ga.nyb, (long long)nblocks,
                    xplan_makespan(xp, nxb, tiles, slots, 2 * (K - 1), U));
@@ -557,10 +577,26 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
   // ranks 0.379 -> 0.359, 2 ranks unchanged (profiles/boundary_slabs_r02.md).
   if (p) {
     const Box& bx = p->box;
+    // 4-plane slabs of a K = 3 sweep before a long sweep (Solver::enqueue_multi
+    // thick): 5-wave tiles of 10 x-rows store all 4 planes in one tile
+    if (K == 3 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && bx.extent(0) == 4 &&
+        bx.extent(1) >= 16 * bx.extent(0)) {
+      if constexpr (sizeof(Real) == 8) launch_tbl<Real, 2, 5, 3, 3, 2, true>(*p, k, s);
+      else launch_tbl<Real, 2, 5, 3, 3, 0, true>(*p, k, s);
+      return true;
+    }
     if (K == 3 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && bx.extent(0) > 0 && bx.extent(0) <= 2 * K &&
         bx.extent(1) >= 16 * bx.extent(0)) {
       if constexpr (sizeof(Real) == 8) launch_tbl<Real, 3, 3, 3, 3, 2, true>(*p, k, s);
       else launch_tbl<Real, 3, 3, 3, 3, 0, true>(*p, k, s);
+      return true;
+    }
+    // the (K+1)-plane boundary slabs of long sweeps across x halos (K = 4):
+    // 4-wave tiles of 12 x-rows store the 4 slab planes
+    if (K == 4 && k.V == 0 && k.R == 0 && k.WY == 0 && k.NT == 0 && bx.extent(0) > 0 && bx.extent(0) <= K &&
+        bx.extent(1) >= 16 * bx.extent(0)) {
+      if constexpr (sizeof(Real) == 8) launch_tbl<Real, 3, 4, 4, 3, 2, true>(*p, k, s);
+      else launch_tbl<Real, 3, 4, 4, 3, 0, true>(*p, k, s);
       return true;
     }
   }

@@ -25,6 +25,10 @@
 // residual is |T^{n+1} - T^n| in fp32 (resid_abs).
 #include <hip/hip_runtime.h>
 
+#include <array>
+#include <map>
+#include <mutex>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -314,7 +318,24 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
 // gain, predicts a shorter sweep, and only for boxes of >= 500 x planes
 // (1022^3: 120 keeps 9 tile columns, 112 would add a 14-wide 10th: 1397 vs
 // 1294 GLUPS).
+static int pair_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L);
 int pair_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L) {
+  // memoised: every eager launch asks
+  static std::mutex mu;
+  static std::map<std::array<int64_t, 8>, int> memo;
+  const std::array<int64_t, 8> key{nx, ny, nz, K, TY, slots, U, L};
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+  }
+  const int zs = pair_z_stride_plan(nx, ny, nz, K, TY, slots, U, L);
+  std::lock_guard<std::mutex> lk(mu);
+  memo[key] = zs;
+  return zs;
+}
+
+static int pair_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L) {
   const int wide = 128 - 2 * K - 2;
   const int aligned = wide & ~15;
   if (aligned == wide || aligned <= 0 || nx < 500) return wide;
@@ -394,7 +415,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
                : 0;
   }();
   HEAT3D_CHECK(spill == 0, "tl pair variant " << ks.str() << " spills " << spill << " B of registers per lane");
-  unsigned long long* r = p.state ? &p.state->residual[p.slot] : nullptr;
+  unsigned long long* r = p.state && p.residual ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
   // spec fields L and ZS as in launch_tbl (L = 0, ZS = 0: the timed schedule of this box)
   auto fire = [&](int zs, int Lx) {

@@ -713,6 +713,8 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("temporal_blocking", &Solver::temporal_blocking)
       .def_property_readonly("temporal_steps", &Solver::temporal_steps)
       .def_property_readonly("field_buffers", &Solver::field_buffers)
+      .def_property_readonly("ghost_depth", &Solver::ghost_depth)
+      .def_property_readonly("long_halo_sweeps", &Solver::long_halo_sweeps)
       .def_property_readonly("backend_name", [](Solver& s) { return std::string(s.backend().name()); })
       .def_property_readonly("comm_name", [](Solver& s) { return std::string(s.comm().name()); })
       .def_property_readonly("comm_size", [](Solver& s) { return s.comm().size(); })

@@ -196,12 +196,12 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   for (const auto& sd : dec_.subs)
     for (int a = 0; a < 3; ++a) min_n[a] = std::min(min_n[a], sd.n[a]);
   const bool block = dims[1] > 1 || dims[2] > 1;
+  const bool has_split = dims[0] * dims[1] * dims[2] > 1;
   bool fits = true;
   for (int a = 0; a < 3; ++a) fits &= dims[a] == 1 || min_n[a] >= K;
   tb_ = kspec_.kind != KernelSpec::Naive && (cfg_.temporal >= 2 || (cfg_.temporal == 0 && be_->is_gpu())) && fits;
   K_ = tb_ ? K : 1;
-  for (int a = 0; a < 3; ++a) hd_[a] = tb_ && dims[a] > 1 ? K : 1;
-  halo_depth_ = hd_[0];
+  for (int a = 0; a < 3; ++a) hd_[a] = xd_[a] = tb_ && dims[a] > 1 ? K : 1;
   ordered_halo_ = tb_ && block;
   // overlapped sweeps need a non-empty interior between the boundary layers
   // of every split axis; otherwise exchange first, then sweep
@@ -215,6 +215,33 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
                      std::to_string(kResidualSlots / 2));
   lag_ = tb_overlap_ && 2 * K_ <= kResidualSlots && cfg_.lag != 0;
   nbuf_ = lag_ ? 3 : 2;
+  // Long sweeps across halos: a step count n = a K + b (K+1) runs as a + b
+  // sweeps instead of ending in a partial sweep of n mod K steps, whose HBM
+  // pass costs nearly a full sweep (fp64 1022^3: K = 2 3.5 ms vs K = 3 3.6 ms)
+  // — the driver's 20-step window at N > 1 is 6 x 3 + 2 otherwise.  Ghosts go
+  // K+1 deep on split axes; only a long sweep exchanges K+1 planes.  Needs
+  // K+1 owned points per split axis (2(K+1)+1 when overlapped), the K+1
+  // kernel, and two banks of K+1 residual slots under the lagged check.
+  {
+    bool ok = tb_ && has_split && cfg_.long_sweeps && K + 1 <= 6 && K + 1 <= kResidualSlots &&
+              (!lag_ || 2 * (K + 1) <= kResidualSlots);
+    for (int a = 0; a < 3; ++a) {
+      ok &= dims[a] == 1 || min_n[a] >= K + 1;
+      if (tb_overlap_) ok &= dims[a] == 1 || min_n[a] >= 2 * (K + 1) + 1;
+    }
+    if (ok && be_->is_gpu()) {
+      KernelSpec ks;
+      ks.kind = kspec2_.kind;
+      ks.K = K + 1;
+      ok = hip::lean_supported(dt_, ks);
+    }
+    long_halo_ = ok;
+    if (long_halo_)
+      for (int a = 0; a < 3; ++a)
+        if (dims[a] > 1) hd_[a] = K + 1;
+    slot_stride_ = K_ + (long_halo_ ? 1 : 0);
+  }
+  halo_depth_ = hd_[0];
   fake_allreduce_us_ = cfg_.fake_allreduce_us;
   chain_ = comm_->ordered_collectives() && !comm_->all_local() && comm_->size() > 1;
   // CU reservation for the overlapped schedule of a real multi-rank job
@@ -248,32 +275,42 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
       u[0] = nlo && hd_[a] > 1 ? -(K_ - 1) : 0;
       u[1] = l.sd.n[a] + (nhi && hd_[a] > 1 ? K_ - 1 : 0);
     }
-    l.tb_interior = l.owned;
-    if (tb_overlap_) {
-      // interior: the owned box minus a K-thick layer on every face with a
-      // neighbour (its K-step update reads no ghost).  Boundary pieces, an
-      // onion: the K-thick layers of axis a span the interior range of the
+    // interior / boundary pieces of the overlapped sweeps of depth d
+    auto pieces = [&](int64_t d, Box* interior, std::vector<Box>* boundary) {
+      *interior = l.owned;
+      boundary->clear();
+      if (!tb_overlap_) return;
+      // interior: the owned box minus a d-thick layer on every face with a
+      // neighbour (its d-step update reads no ghost).  Boundary pieces, an
+      // onion: the d-thick layers of axis a span the interior range of the
       // axes before a and the full range of the axes after it — disjoint,
       // and together with the interior they tile the owned box.
       bool nb[3][2];
       for (int a = 0; a < 3; ++a)
         for (int e = 0; e < 2; ++e) nb[a][e] = hd_[a] > 1 && l.sd.has_neighbor(static_cast<Face>(2 * a + e));
       for (int a = 0; a < 3; ++a) {
-        if (nb[a][0]) l.tb_interior.lo[a] = K_;
-        if (nb[a][1]) l.tb_interior.hi[a] = l.sd.n[a] - K_;
+        if (nb[a][0]) interior->lo[a] = d;
+        if (nb[a][1]) interior->hi[a] = l.sd.n[a] - d;
       }
       for (int a = 0; a < 3; ++a)
         for (int side = 0; side < 2; ++side) {
           if (!nb[a][side]) continue;
           Box b = l.owned;
           for (int c = 0; c < a; ++c) {
-            b.lo[c] = l.tb_interior.lo[c];
-            b.hi[c] = l.tb_interior.hi[c];
+            b.lo[c] = interior->lo[c];
+            b.hi[c] = interior->hi[c];
           }
-          b.lo[a] = side ? l.sd.n[a] - K_ : 0;
-          b.hi[a] = b.lo[a] + K_;
-          l.tb_boundary.push_back(b);
+          b.lo[a] = side ? l.sd.n[a] - d : 0;
+          b.hi[a] = b.lo[a] + d;
+          boundary->push_back(b);
         }
+    };
+    pieces(K_, &l.tb_interior, &l.tb_boundary);
+    if (long_halo_) {
+      pieces(K_ + 1, &l.tb_interior_long, &l.tb_boundary_long);
+    } else {  // long sweeps of a single subdomain (no ghosts to widen into)
+      l.tb_interior_long = l.tb_interior;
+      l.tb_boundary_long = l.tb_boundary;
     }
     local_.push_back(l);
   }
@@ -363,24 +400,39 @@ void Solver::setup_faces() {
       io.face = face;
       io.peer = l.sd.neighbors[f];
       const int a = face_axis(face), side = face_side(face);
-      for (int b = 0; b < 3; ++b) {
-        io.send_box.lo[b] = io.recv_box.lo[b] = 0;
-        io.send_box.hi[b] = io.recv_box.hi[b] = l.sd.n[b];
-      }
-      const int64_t dep = hd_[a];
-      io.send_box.lo[a] = side ? l.sd.n[a] - dep : 0;
-      io.send_box.hi[a] = io.send_box.lo[a] + dep;
-      io.recv_box.lo[a] = side ? l.sd.n[a] : -dep;
-      io.recv_box.hi[a] = io.recv_box.lo[a] + dep;
-      if (ordered_halo_) {
-        // axis-ordered exchange (x, then y, then z): a face of axis a also
-        // carries the deep ghosts of the axes before it, which the earlier
-        // phases have filled, so edges and corners arrive in the right order
-        for (int b = 0; b < a; ++b) {
-          const int64_t elo = l.sd.has_neighbor(static_cast<Face>(2 * b)) ? hd_[b] : 0;
-          const int64_t ehi = l.sd.has_neighbor(static_cast<Face>(2 * b + 1)) ? hd_[b] : 0;
-          io.send_box.lo[b] = io.recv_box.lo[b] = -elo;
-          io.send_box.hi[b] = io.recv_box.hi[b] = l.sd.n[b] + ehi;
+      for (int dv = 0; dv < 2; ++dv) {
+        // exchange depth: the regular one, or the ghost depth (K+1 with long_halo_)
+        auto depth = [&](int b) { return dv ? hd_[b] : xd_[b]; };
+        FaceGeom& fg = io.g[dv];
+        for (int b = 0; b < 3; ++b) {
+          fg.send_box.lo[b] = fg.recv_box.lo[b] = 0;
+          fg.send_box.hi[b] = fg.recv_box.hi[b] = l.sd.n[b];
+        }
+        const int64_t dep = depth(a);
+        fg.send_box.lo[a] = side ? l.sd.n[a] - dep : 0;
+        fg.send_box.hi[a] = fg.send_box.lo[a] + dep;
+        fg.recv_box.lo[a] = side ? l.sd.n[a] : -dep;
+        fg.recv_box.hi[a] = fg.recv_box.lo[a] + dep;
+        if (ordered_halo_) {
+          // axis-ordered exchange (x, then y, then z): a face of axis a also
+          // carries the deep ghosts of the axes before it, which the earlier
+          // phases have filled, so edges and corners arrive in the right order
+          for (int b = 0; b < a; ++b) {
+            const int64_t elo = l.sd.has_neighbor(static_cast<Face>(2 * b)) ? depth(b) : 0;
+            const int64_t ehi = l.sd.has_neighbor(static_cast<Face>(2 * b + 1)) ? depth(b) : 0;
+            fg.send_box.lo[b] = fg.recv_box.lo[b] = -elo;
+            fg.send_box.hi[b] = fg.recv_box.hi[b] = l.sd.n[b] + ehi;
+          }
+        }
+        if (a == 0) {
+          // x faces: whole planes (ghost rows and padding included) are
+          // contiguous; the neighbour across an x face has the same ny, nz and
+          // therefore the same strides.
+          fg.send_off = l.L.plane_offset(fg.send_box.lo[0]);
+          fg.recv_off = l.L.plane_offset(fg.recv_box.lo[0]);
+          fg.elems = dep * l.L.sx;
+        } else {
+          fg.elems = fg.send_box.volume();
         }
       }
       if (comm_->all_local()) {
@@ -388,18 +440,10 @@ void Solver::setup_faces() {
           if (local_[q].sd.rank == io.peer) io.peer_local = (int)q;
         HEAT3D_CHECK(io.peer_local >= 0, "local neighbour not found");
       } else if (a == 0) {
-        // x faces: whole planes (ghost rows and padding included) are
-        // contiguous; the neighbour across an x face has the same ny, nz and
-        // therefore the same strides.
         io.contiguous = true;
-        const int64_t si = io.send_box.lo[0], ri = io.recv_box.lo[0];
-        io.send_off = l.L.plane_offset(si);
-        io.recv_off = l.L.plane_offset(ri);
-        io.elems = dep * l.L.sx;
       } else {
-        io.elems = io.send_box.volume();
-        io.sendbuf = be_->alloc(io.elems * esize_);
-        io.recvbuf = be_->alloc(io.elems * esize_);
+        io.sendbuf = be_->alloc(io.g[1].elems * esize_);
+        io.recvbuf = be_->alloc(io.g[1].elems * esize_);
       }
       l.faces.push_back(io);
     }
@@ -462,6 +506,7 @@ void Solver::initialize() {
   cur_ = 0;
   nsweep_ = 0;
   last_kind_ = 0;
+  last_bnd_ = 0;
   segs_.clear();
   seg_head_ = 0;
   if (!cfg_.restart.empty()) load_checkpoint(cfg_.restart);
@@ -492,7 +537,7 @@ void Solver::tune_schedules() {
   const bool on = cfg_.autotune > 0 || (cfg_.autotune < 0 && !has_halo_ && local_.size() == 1);
   if (!on || !tb_ || !be_->is_gpu()) return;
   std::vector<KernelSpec> specs{kspec2_};
-  if (!has_halo_ && cfg_.long_sweeps && K_ + 1 <= 6 && K_ + 1 <= kResidualSlots) {
+  if ((!has_halo_ || long_halo_) && cfg_.long_sweeps && K_ + 1 <= 6 && K_ + 1 <= kResidualSlots) {
     KernelSpec ks;
     ks.kind = kspec2_.kind;
     ks.K = K_ + 1;
@@ -501,12 +546,13 @@ void Solver::tune_schedules() {
   for (const KernelSpec& ks : specs) {
     const int Kp = ks.K;
     for (auto& l : local_) {
-      if (l.tb_interior.empty()) continue;
+      const Box& box = Kp > K_ ? l.tb_interior_long : l.tb_interior;
+      if (box.empty()) continue;
       StencilParams sp;
       sp.in = l.field[0];
       sp.out = l.field[nxt(0)];
       sp.L = l.L;
-      sp.box = l.tb_interior;
+      sp.box = box;
       for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
       sp.state = nullptr;
       sp.cu_reserved = be_->reserved_cus();
@@ -525,7 +571,14 @@ void Solver::tune_schedules() {
 }
 
 int Solver::preheat(int sweeps) {
-  if (!tb_ || !be_->is_gpu() || sweeps <= 0) return 0;
+  if (!tb_ || sweeps <= 0) return 0;
+  // Ordered behind every issued sweep and convergence check (join_pipeline),
+  // the warm-up sweeps carry the device done flag without residual slots
+  // (StencilParams::residual = false): once any issued iteration has met the
+  // criterion they are no-ops, so nxt(cur()) — with two buffers the input of
+  // the last sweep, which finalize_converged() needs for the rollback — is
+  // only rewritten while no rollback can need it, and then with the values
+  // the next sweep writes there anyway (a sweep is idempotent).
   join_pipeline();
   const int Kp = K_;
   int n = 0;
@@ -538,7 +591,8 @@ int Solver::preheat(int sweeps) {
       sp.L = l.L;
       sp.box = l.tb_interior;
       for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
-      sp.state = nullptr;
+      sp.state = dstate_;
+      sp.residual = false;
       sp.cu_reserved = be_->reserved_cus();
       auto shrink = [&](const int64_t (&u)[2], int64_t nn, int64_t (&o)[2]) {
         o[0] = u[0] < 0 ? -(Kp - 1) : u[0];
@@ -551,13 +605,17 @@ int Solver::preheat(int sweeps) {
       ++n;
     }
   }
-  // the next sweep's inputs and events are as they were: later work orders
-  // behind the preheat through the compute stream
+  // the next sweep's inputs and events are as they were; every stream orders
+  // its later work behind the preheat (its output planes overlap the next
+  // sweep's boundary slabs, which write the same values)
+  ev_record(EV_FORK, kCompute);
+  ev_wait(kComm, EV_FORK);
+  ev_wait(kReduce, EV_FORK);
   return n;
 }
 
 // --- one iteration -----------------------------------------------------------
-void Solver::enqueue_halo(int p, StreamId s) {
+void Solver::enqueue_halo(int p, StreamId s, int dv) {
   // p = buffer index whose faces / ghosts are exchanged
   be_->range_push("halo");
   prof_record(prof_idx_, PE_HALO0, s);
@@ -566,14 +624,14 @@ void Solver::enqueue_halo(int p, StreamId s) {
   const int nphase = ordered_halo_ ? 3 : 1;
   for (int ph = 0; ph < nphase; ++ph) {
     auto in_phase = [&](const FaceIO& io) { return !ordered_halo_ || face_axis(io.face) == ph; };
-    enqueue_halo_phase(p, s, in_phase);
+    enqueue_halo_phase(p, s, dv, in_phase);
   }
   prof_record(prof_idx_, PE_HALO1, s);
   be_->range_pop();
 }
 
 template <typename Pred>
-void Solver::enqueue_halo_phase(int p, StreamId s, Pred in_phase) {
+void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase) {
   if (comm_->all_local()) {
     for (auto& l : local_)
       for (auto& io : l.faces) {
@@ -581,9 +639,9 @@ void Solver::enqueue_halo_phase(int p, StreamId s, Pred in_phase) {
         const Local& nb = local_[io.peer_local];
         const Box* src = nullptr;
         for (auto& nio : nb.faces)
-          if (nio.face == opposite(io.face)) src = &nio.send_box;
+          if (nio.face == opposite(io.face)) src = &nio.g[dv].send_box;
         HEAT3D_CHECK(src, "opposite face missing");
-        be_->copy_box(dt_, nb.field[p], nb.L, *src, l.field[p], l.L, io.recv_box, s);
+        be_->copy_box(dt_, nb.field[p], nb.L, *src, l.field[p], l.L, io.g[dv].recv_box, s);
       }
   } else {
     std::vector<Transfer> xs;
@@ -591,16 +649,17 @@ void Solver::enqueue_halo_phase(int p, StreamId s, Pred in_phase) {
       char* base = static_cast<char*>(l.field[p]);
       for (auto& io : l.faces) {
         if (!in_phase(io)) continue;
-        if (!io.contiguous) be_->pack_box(dt_, l.field[p], l.L, io.send_box, io.sendbuf, s);
+        const FaceGeom& fg = io.g[dv];
+        if (!io.contiguous) be_->pack_box(dt_, l.field[p], l.L, fg.send_box, io.sendbuf, s);
         Transfer snd, rcv;
         snd.src_rank = l.sd.rank;
         snd.dst_rank = io.peer;
-        snd.src = io.contiguous ? base + io.send_off * esize_ : io.sendbuf;
-        snd.bytes = io.elems * esize_;
+        snd.src = io.contiguous ? base + fg.send_off * esize_ : io.sendbuf;
+        snd.bytes = fg.elems * esize_;
         rcv.src_rank = io.peer;
         rcv.dst_rank = l.sd.rank;
-        rcv.dst = io.contiguous ? base + io.recv_off * esize_ : io.recvbuf;
-        rcv.bytes = io.elems * esize_;
+        rcv.dst = io.contiguous ? base + fg.recv_off * esize_ : io.recvbuf;
+        rcv.bytes = fg.elems * esize_;
         xs.push_back(snd);
         xs.push_back(rcv);
       }
@@ -613,7 +672,7 @@ void Solver::enqueue_halo_phase(int p, StreamId s, Pred in_phase) {
     }
     for (auto& l : local_)
       for (auto& io : l.faces)
-        if (in_phase(io) && !io.contiguous) be_->unpack_box(dt_, l.field[p], l.L, io.recv_box, io.recvbuf, s);
+        if (in_phase(io) && !io.contiguous) be_->unpack_box(dt_, l.field[p], l.L, io.g[dv].recv_box, io.recvbuf, s);
   }
 }
 
@@ -713,19 +772,24 @@ void Solver::enqueue_iteration(int p, int bi) {
 // under sweep q+1, whose residuals go to the other slot bank; if sweep q
 // converged, q+1 was speculative (its output buffer is not q's input) and
 // q+2 onwards are no-ops.  Exchanged values stay bitwise identical.
-void Solver::enqueue_multi(int bi, int Kp) {
+void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   // Kp < K_: a partial sweep of Kp steps (the remainder of a step count that
   // is not a multiple of K_), same schedule and buffers, kernel of depth Kp;
-  // Kp = K_ + 1: a long sweep (long_sweeps_for, single subdomain only)
+  // Kp = K_ + 1: a long sweep (long_sweeps_for: single subdomain, or K+1-deep
+  // ghosts with long_halo_), whose exchange and boundary layers are K+1 deep
   if (Kp <= 0) Kp = K_;
-  HEAT3D_CHECK(Kp <= K_ || (Kp == K_ + 1 && !has_halo_), "sweep depth " << Kp << " exceeds the halo depth " << K_);
+  HEAT3D_CHECK(Kp <= K_ || (Kp == K_ + 1 && (!has_halo_ || long_halo_)),
+               "sweep depth " << Kp << " exceeds the halo depth " << K_);
+  const int dv = Kp > K_ ? 1 : 0;
+  // boundary pieces K+1 deep for long sweeps and for the sweep before one
+  const bool lb = dv || (thick && long_halo_);
   H3D_TRACE("sweep" << Kp << " issued=" << issued_ << " buf=" << bi << (capturing_ ? " (capturing)" : ""));
   HEAT3D_CHECK(tb_, "temporal blocking not enabled for this decomposition");
   if (last_kind_ != 2) join_pipeline();
   last_kind_ = 2;
   // lagged schedule: events and residual slots alternate by sweep parity
   const int q = lag_ ? (int)(nsweep_ & 1) : bi;
-  const int slot0 = lag_ ? q * K_ : 0;
+  const int slot0 = lag_ ? q * slot_stride_ : 0;
   KernelSpec ks = kspec2_;
   if (Kp != K_) {
     // partial (Kp < K) or long (Kp = K + 1, single subdomain) sweep: the
@@ -757,10 +821,10 @@ void Solver::enqueue_multi(int bi, int Kp) {
   if (!tb_overlap_) {
     ev_wait(kCompute, EV_CHK + 0);
     ev_wait(kCompute, EV_CHK + 1);
-    if (has_halo_) enqueue_halo(bi, kCompute);
+    if (has_halo_) enqueue_halo(bi, kCompute, dv);
     be_->range_push("sweep");
     prof_record(prof_idx_, PE_INT0, kCompute);
-    for (auto& l : local_) be_->sweep(dt_, params(l, l.tb_interior), ks, kCompute);
+    for (auto& l : local_) be_->sweep(dt_, params(l, dv ? l.tb_interior_long : l.tb_interior), ks, kCompute);
     prof_record(prof_idx_, PE_INT1, kCompute);
     be_->range_pop();
     prof_record(prof_idx_, PE_RED0, kCompute);
@@ -789,14 +853,20 @@ void Solver::enqueue_multi(int bi, int Kp) {
   // sweep's interior; the deferred all-reduce + check follow it.  Without the
   // lag this sweep's interior waits for that check (chk_prev), so it is issued
   // after the flush.
-  enqueue_halo(bi, kComm);
+  // the halo sends the owned planes [0, d) / [n-d, n) of T^t, written by the
+  // previous sweep's boundary slabs (comm-stream order) — unless they were
+  // thinner than d, when the previous interior wrote the rest: wait for it
+  // (a long sweep right after a K-thick one, e.g. across step() calls)
+  if (last_bnd_ > 0 && (dv ? K_ + 1 : K_) > last_bnd_) ev_wait(kComm, EV_INT + (q ^ 1));
+  last_bnd_ = lb ? K_ + 1 : K_;
+  enqueue_halo(bi, kComm, dv);
   flush_pending_reduce();
   // [A] interior planes
   ev_wait(kCompute, EV_CHK + chk_prev);
   ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of our input
   be_->range_push("interior");
   prof_record(prof_idx_, PE_INT0, kCompute);
-  for (auto& l : local_) be_->sweep(dt_, params(l, l.tb_interior), ks, kCompute);
+  for (auto& l : local_) be_->sweep(dt_, params(l, lb ? l.tb_interior_long : l.tb_interior), ks, kCompute);
   prof_record(prof_idx_, PE_INT1, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
@@ -806,7 +876,7 @@ void Solver::enqueue_multi(int bi, int Kp) {
   be_->range_push("boundary");
   prof_record(prof_idx_, PE_BND0, kComm);
   for (auto& l : local_) {
-    for (const Box& b : l.tb_boundary) be_->sweep(dt_, params(l, b), ks, kComm);
+    for (const Box& b : lb ? l.tb_boundary_long : l.tb_boundary) be_->sweep(dt_, params(l, b), ks, kComm);
   }
   prof_record(prof_idx_, PE_BND1, kComm);
   be_->range_pop();
@@ -1023,7 +1093,7 @@ int Solver::graph_len_for(int64_t n) const {
 }
 
 int Solver::long_sweeps_for(int64_t n) const {
-  if (!tb_ || has_halo_ || !kspec2_.multi_step() || n % K_ == 0) return 0;
+  if (!tb_ || (has_halo_ && !long_halo_) || !kspec2_.multi_step() || n % K_ == 0) return 0;
   if (K_ + 1 > 6 || K_ + 1 > kResidualSlots) return 0;
   const int64_t b = n % K_;             // n = a K + b (K + 1) with a = (n - b (K + 1)) / K
   if (b * (K_ + 1) > n) return 0;
@@ -1084,7 +1154,7 @@ Solver::GraphEntry* Solver::build_graph(int G) {
   Event saved_cur[EV_COUNT];
   std::memcpy(saved_cur, cur_ev_, sizeof(saved_cur));
   const int64_t s_issued = issued_, s_nsweep = nsweep_;
-  const int s_cur = cur_, s_last = last_kind_;
+  const int s_cur = cur_, s_last = last_kind_, s_bnd = last_bnd_;
   const std::size_t need = 16 * (std::size_t)G + 16;
   while (cap_pool_.size() < need) cap_pool_.push_back(be_->event_create());
   cap_next_ = 0;
@@ -1136,6 +1206,7 @@ Solver::GraphEntry* Solver::build_graph(int G) {
   nsweep_ = s_nsweep;
   cur_ = s_cur;
   last_kind_ = s_last;
+  last_bnd_ = s_bnd;
   pending_.valid = false;
   std::memcpy(ev_valid_, saved, sizeof(saved));
   std::memcpy(cur_ev_, saved_cur, sizeof(saved_cur));
@@ -1188,6 +1259,7 @@ void Solver::run_chunk(int64_t n) {
         }
         n -= G;
         last_kind_ = g->kind;
+        last_bnd_ = 0;  // the graph ends joined into the compute stream (re-fork below)
         // the graph joined every stream into compute: re-fork for eager work
         for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
         ev_record(EV_FORK, kCompute);
@@ -1200,7 +1272,7 @@ void Solver::run_chunk(int64_t n) {
       // a full sweep, or a partial one for a remainder of 2 .. K-1 steps
       const int Kp = (int)std::min<int64_t>(n, K_);
       record_segment(issued_, Kp, cur());
-      enqueue_multi(cur(), Kp);
+      enqueue_multi(cur(), Kp, nlong > 0 && n == Kp);
       issued_ += Kp;
       cur_ = nxt(cur_);
       n -= Kp;
@@ -1266,6 +1338,8 @@ RunResult Solver::run() {
   int64_t next_verify = cfg_.verify_halo > 0 ? issued_ + cfg_.verify_halo : -1;
   if (cfg_.timers) set_phase_timing(true);
   int64_t printed = issued_;
+  const int64_t iter0 = issued_;
+  double last_beat = t0;
   const double watchdog = cfg_.watchdog_s;
   while (issued_ < cfg_.iter_max && !stop) {
     int64_t n = std::min(K, cfg_.iter_max - issued_);
@@ -1295,6 +1369,16 @@ RunResult Solver::run() {
         printed = hs.iter;
       }
       if (hs.done) stop = true;
+      if (cfg_.progress_s > 0 && is_root() && now_s() - last_beat >= cfg_.progress_s) {
+        // heartbeat: long convergence runs (1024^3 at eps 1e-5: ~2e5
+        // iterations) stay visibly alive to launchers that kill silent jobs
+        last_beat = now_s();
+        const double el = last_beat - t0;
+        std::fprintf(stderr, "heat3d: progress iteration %lld residual %.6e relative %.6e (eps %.3e) %.1f s, %.1f GLUPS\n",
+                     (long long)hs.iter, hs.last_residual, hs.norm > 0 ? hs.last_residual / hs.norm : 0.0, hs.eps, el,
+                     el > 0 ? (double)interior_points() * (double)(hs.iter - iter0) / el / 1e9 : 0.0);
+        std::fflush(stderr);
+      }
     }
     have_prev = true;
     pslot ^= 1;
@@ -1791,11 +1875,26 @@ void Solver::load_checkpoint(const std::string& dir) {
     void* stage = be_->alloc(host.size());
     for (int64_t x0 = 0; x0 < lb.extent(0); x0 += xc) {
       const int64_t nx = std::min(xc, lb.extent(0) - x0);
+      // reads: whole rows are contiguous runs of the file once the box spans
+      // z (one read per plane), and whole planes once it spans y too (one
+      // read per chunk); otherwise one read per row
+      const int64_t gi0 = l.sd.gstart[0] - 1 + x0, gj0 = l.sd.gstart[1] - 1, gk0 = l.sd.gstart[2] - 1;
+      if (ez == N[2] && ey == N[1]) {
+        io::pread_all(fd, host.data(), nx * plane * esize_, gi0 * N[1] * N[2] * esize_);
+      } else if (ez == N[2]) {
+        for (int64_t i = 0; i < nx; ++i)
+          io::pread_all(fd, host.data() + i * plane * esize_, plane * esize_,
+                        ((gi0 + i) * N[1] + gj0) * N[2] * esize_);
+      } else {
+        for (int64_t i = 0; i < nx; ++i)
+          for (int64_t j = 0; j < ey; ++j)
+            io::pread_all(fd, host.data() + (i * ey + j) * ez * esize_, ez * esize_,
+                          (((gi0 + i) * N[1] + gj0 + j) * N[2] + gk0) * esize_);
+      }
       for (int64_t i = 0; i < nx; ++i)
         for (int64_t j = 0; j < ey; ++j) {
-          const int64_t gi = l.sd.gstart[0] - 1 + x0 + i, gj = l.sd.gstart[1] - 1 + j, gk = l.sd.gstart[2] - 1;
+          const int64_t gi = gi0 + i, gj = gj0 + j, gk = gk0;
           char* row = host.data() + (i * ey + j) * ez * esize_;
-          io::pread_all(fd, row, ez * esize_, ((gi * N[1] + gj) * N[2] + gk) * esize_);
           // checksum over this rank's extended box only (a partition of the grid)
           if (gi >= ext.lo[0] && gi < ext.hi[0] && gj >= ext.lo[1] && gj < ext.hi[1]) {
             const int64_t k0 = ext.lo[2] - gk, k1 = ext.hi[2] - gk;
@@ -1844,8 +1943,9 @@ int Solver::verify_halos() {
   int q = 0;
   for (auto& l : local_)
     for (auto& io : l.faces) {
-      be_->box_bitsum(dt_, l.field[p], l.L, io.send_box, dsum + 2 * q, kCompute);
-      be_->box_bitsum(dt_, l.field[p], l.L, io.recv_box, dsum + 2 * q + 1, kCompute);
+      // the regular depth: every exchange carries at least these planes
+      be_->box_bitsum(dt_, l.field[p], l.L, io.g[0].send_box, dsum + 2 * q, kCompute);
+      be_->box_bitsum(dt_, l.field[p], l.L, io.g[0].recv_box, dsum + 2 * q + 1, kCompute);
       ++q;
     }
   be_->sync(kCompute);
@@ -1939,6 +2039,18 @@ std::unique_ptr<Solver> make_solver_from_env(const Config& cfg) {
   // MASTER_PORT; bootstrap on MASTER_PORT + 1 unless told otherwise.
   w.bootstrap_port = env_int("HEAT3D_BOOTSTRAP_PORT", nullptr, env_int("MASTER_PORT", nullptr, 29500) + 1);
   w.device = cfg.device;
+  const char* sp = std::getenv("HEAT3D_SHOW_PLACEMENT");
+  if (sp && *sp && sp[0] != '0') {
+    // where the launcher's variables put this rank (tests: mpirun / torchrun contracts)
+    const char* src = std::getenv("LOCAL_RANK")                   ? "LOCAL_RANK"
+                      : std::getenv("OMPI_COMM_WORLD_LOCAL_RANK") ? "OMPI_COMM_WORLD_LOCAL_RANK"
+                      : std::getenv("MPI_LOCALRANKID")            ? "MPI_LOCALRANKID"
+                                                                  : "rank";
+    const int n = cfg.backend == BackendKind::Cpu ? 0 : hip_device_count();
+    const int dev = w.device >= 0 ? w.device : (n > 0 ? w.local_rank % n : -1);
+    std::fprintf(stderr, "heat3d: placement rank=%d size=%d local_rank=%d from=%s device=%d of %d\n", w.rank, w.size,
+                 w.local_rank, src, dev, n);
+  }
   return make_solver(cfg, w);
 }
 

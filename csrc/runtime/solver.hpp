@@ -126,6 +126,10 @@ class Solver {
   int temporal_steps() const { return K_; }
   // field buffers per subdomain (3 = lagged convergence check of overlapped sweeps)
   int field_buffers() const { return nbuf_; }
+  // ghost depth per axis (K on split axes with temporal blocking, K+1 when
+  // long sweeps cross the halos) and whether they do
+  std::array<int64_t, 3> ghost_depth() const { return {hd_[0], hd_[1], hd_[2]}; }
+  bool long_halo_sweeps() const { return long_halo_; }
   // HBM preflight (constructor): bytes this solver allocates for its local
   // ranks (fields + face staging), and the backend's free / total memory
   // just before those allocations (0 when the backend cannot tell)
@@ -169,13 +173,19 @@ class Solver {
   void inject(int local_idx, int64_t i, int64_t j, int64_t k, double value, bool previous = false);
 
  private:
+  // One face's exchange at one halo depth: the K-plane halo of regular
+  // sweeps (dv = 0), the (K+1)-plane halo of long sweeps (dv = 1; the same as
+  // dv = 0 without long_halo_).  Boxes in local coordinates.
+  struct FaceGeom {
+    Box send_box, recv_box;
+    int64_t send_off = 0, recv_off = 0, elems = 0;  // contiguous x faces: in place
+  };
   struct FaceIO {
     Face face;
     int peer;
-    Box send_box, recv_box;     // local coords
+    FaceGeom g[2];
     bool contiguous = false;    // x faces: whole planes sent in place
-    int64_t send_off = 0, recv_off = 0, elems = 0;
-    void* sendbuf = nullptr;    // staging for packed faces
+    void* sendbuf = nullptr;    // staging for packed faces (sized for the deepest halo)
     void* recvbuf = nullptr;
     int peer_local = -1;        // LocalComm: index of the neighbour in local_
   };
@@ -190,6 +200,9 @@ class Solver {
     // (need no halo), K-plane boundary slabs, u range widened into the halos
     Box tb_interior;
     std::vector<Box> tb_boundary;
+    // the same for long sweeps of depth K+1 across halos (long_halo_)
+    Box tb_interior_long;
+    std::vector<Box> tb_boundary_long;
     int64_t ux[2] = {0, -1};
     int64_t uy[2] = {0, -1}, uz[2] = {0, -1};  // y / z update ranges (deep y / z halos)
   };
@@ -198,10 +211,15 @@ class Solver {
   // one single-step iteration: residual slot / event parity p, input buffer bi
   void enqueue_iteration(int p, int bi);
   // K iterations in one temporally blocked sweep from buffer bi
-  void enqueue_multi(int bi, int Kp = 0);
-  void enqueue_halo(int bi, StreamId s);
+  // thick: boundary layers K+1 deep (the long sweeps' pieces) for a K-step
+  // sweep that a long sweep follows (its K+1-deep halo sends the planes
+  // this sweep writes, which must come from the boundary slabs, not the
+  // interior the halo does not wait for)
+  void enqueue_multi(int bi, int Kp = 0, bool thick = false);
+  // dv: halo depth variant (FaceGeom), 1 = the K+1 planes of a long sweep
+  void enqueue_halo(int bi, StreamId s, int dv = 0);
   template <typename Pred>
-  void enqueue_halo_phase(int bi, StreamId s, Pred in_phase);
+  void enqueue_halo_phase(int bi, StreamId s, int dv, Pred in_phase);
   void join_pipeline();      // every stream waits for every pipeline event
   // Collective ordering chain (ordered_collectives comms, > 1 rank): every
   // exchange / all-reduce waits for the previous one's completion event, so
@@ -253,8 +271,15 @@ class Solver {
   bool has_halo_ = false;  // any face with a neighbour on any local subdomain
   bool overlap_ = true;
   bool tb_overlap_ = false;   // sweeps: interior || (deep halo -> boundary slabs)
-  int halo_depth_ = 1;        // x-face halo planes (K with temporal blocking)
-  int64_t hd_[3] = {1, 1, 1}; // halo depth per axis (K on split axes with temporal blocking)
+  int halo_depth_ = 1;        // x-face ghost planes (K, or K+1 with long_halo_)
+  int64_t hd_[3] = {1, 1, 1}; // ghost depth per axis (K on split axes with temporal blocking, K+1 with long_halo_)
+  int64_t xd_[3] = {1, 1, 1}; // regular exchange depth per axis (K on split axes with temporal blocking)
+  // Long sweeps (depth K+1) across halos: ghosts allocated K+1 deep on split
+  // axes, exchanged K+1 deep before a long sweep only; step counts that are
+  // not multiples of K end in long sweeps instead of a partial K-1 sweep
+  bool long_halo_ = false;
+  int slot_stride_ = 1;       // residual slots per sweep bank of the lagged schedule
+  int last_bnd_ = 0;          // boundary-layer depth of the last overlapped sweep (0: none pending)
   bool ordered_halo_ = false; // axis-ordered exchange filling edges / corners (deep y / z halos)
   int last_kind_ = 0;         // 1 = single step, 2 = pair: last enqueued schedule
   DType dt_;

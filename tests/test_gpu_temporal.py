@@ -207,6 +207,16 @@ def test_sweep_thin_slab_y_marching(h3d, gpu, kernel, dtype, n0, box_x, side, ny
     _deep_halo_case(h3d, gpu, kernel, dtype, n0, box_x, side, ny)
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("n0,box_x,side,ny", [(12, (0, 4), "both", 64), (12, (8, 12), "both", 64),
+                                               (9, (0, 4), "lo", 100), (9, (5, 9), "hi", 70),
+                                               (20, (0, 3), "both", 70), (20, (16, 20), "both", 63)])
+def test_sweep_thin_slab_y_marching_k4(h3d, gpu, dtype, n0, box_x, side, ny):
+    """The (K+1)-plane boundary slabs of long sweeps across x halos: K = 4
+    y-marching tiles of 12 x-rows (ny < 16 x planes: the x-marching default)."""
+    _deep_halo_case(h3d, gpu, "tl4", dtype, n0, box_x, side, ny)
+
+
 def _deep_halo_case(h3d, gpu, kernel, dtype, n0, box_x, side, ny=37):
     ops = h3d.ops
     head = kernel.split(":")[0]
@@ -435,3 +445,89 @@ def test_temporal_k5_remainders(h3d, gpu, dtype, iters):
     ra, rb = a.run(), b.run()
     assert ra["iterations"] == rb["iterations"] == iters and ra["last_residual"] == rb["last_residual"]
     assert np.array_equal(a.gather(), b.gather())
+
+
+PREHEAT_GPU = [(1, (1, 1, 1)), (3, (3, 1, 1)), (8, (2, 2, 2))]
+
+
+@pytest.mark.parametrize("vr,dims", PREHEAT_GPU)
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_preheat_state_neutral_gpu(h3d, gpu, vr, dims, dtype):
+    """bench.py's preheat between the warm-up and the timed window:
+    step(a); preheat(n); step(b) == step(a + b) bit for bit (field, residual,
+    iteration count), graphs on, single domain / slabs (3 buffers) / 2x2x2."""
+    n = (45, 61, 150)
+    mk = lambda: h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims,
+                                graph_chunk=12)
+    for a_steps, b_steps in ((5, 20), (6, 12)):
+        a, b = mk(), mk()
+        a.initialize(), b.initialize()
+        a.step(a_steps)
+        a.prepare_steps(b_steps)
+        assert a.native.preheat(5) == 5 * vr
+        a.step(b_steps)
+        b.step(a_steps + b_steps)
+        a.synchronize(), b.synchronize()
+        sa, sb = a.native.state(), b.native.state()
+        assert sa["iter"] == sb["iter"] == a_steps + b_steps
+        assert sa["last_residual"] == sb["last_residual"]
+        assert np.array_equal(a.gather(), b.gather()), (vr, dtype, a_steps)
+
+
+@pytest.mark.parametrize("vr,dims", PREHEAT_GPU)
+def test_preheat_keeps_rollback_input_gpu(h3d, gpu, vr, dims):
+    """Preheat after the converged sweep is a no-op (device done flag): the
+    rollback input survives and run() ends on the same iteration and field."""
+    n = (33, 33, 33)
+    for eps in (1e-3, 9e-4, 8e-4):
+        ref = h3d.HeatSolver(n, 10 ** 6, eps, backend="hip", virtual_ranks=vr, decomp=dims,
+                             extra_args=["--check-every", "6"])
+        rr = ref.run()
+        c = rr["conv_iter"]
+        end = (c // 3 + 1) * 3
+        for extra_sweeps in (0, 1):
+            s = h3d.HeatSolver(n, 10 ** 6, eps, backend="hip", virtual_ranks=vr, decomp=dims,
+                               extra_args=["--check-every", "6"])
+            s.initialize()
+            s.step(end + 3 * extra_sweeps)
+            s.native.preheat(4)
+            r = s.run()
+            assert r["converged"] and r["conv_iter"] == c, (eps, r, c)
+            assert np.array_equal(s.gather(), ref.gather()), (vr, eps, extra_sweeps)
+
+
+@pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (8, 1, 1)), (8, (2, 2, 2)), (4, (1, 2, 2))])
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype):
+    """The driver's window at N > 1 (warm-up 5, then 20 steps = 4 x 3 + 2 x 4):
+    long K+1 sweeps across the halos, including the (K+1)-plane boundary
+    slabs (y-marching K = 4 thin-slab tiles), bitwise equal to single steps."""
+    n = (82, 70, 150)
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims)
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
+    assert a.native.long_halo_sweeps
+    a.initialize(), b.initialize()
+    for k in (5, 20, 11, 4):
+        a.step(k)
+        b.step(k)
+        a.synchronize(), b.synchronize()
+        sa, sb = a.native.state(), b.native.state()
+        assert sa["iter"] == sb["iter"] and sa["last_residual"] == sb["last_residual"]
+        assert np.array_equal(a.gather(), b.gather()), (vr, dims, dtype, k)
+    assert a.native.verify_halos() == 0
+
+
+@pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (2, 2, 2))])
+def test_long_sweep_across_halos_rollback_gpu(h3d, gpu, vr, dims):
+    n = (33, 33, 33)
+    for eps in (1e-3, 9e-4, 8e-4):
+        ref = h3d.HeatSolver(n, 10 ** 6, eps, backend="hip", extra_args=["--temporal", "1"])
+        rr = ref.run()
+        c = rr["conv_iter"]
+        for j in (c // 3, c // 3 - 1):
+            s = h3d.HeatSolver(n, 10 ** 6, eps, backend="hip", virtual_ranks=vr, decomp=dims)
+            s.initialize()
+            s.step(3 * j + 8)
+            r = s.run()
+            assert r["converged"] and r["conv_iter"] == c, (eps, j, r, c)
+            assert np.array_equal(s.gather(), ref.gather()), (vr, eps, j)

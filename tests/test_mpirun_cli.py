@@ -11,6 +11,7 @@ iteration is the single-domain golden (decomposition-independent results),
 and a wrong argument count prints the usage once and fails every rank.
 """
 import os
+import re
 import shutil
 import subprocess
 
@@ -61,3 +62,36 @@ def test_mpirun_usage_error(heat3d_bin, tmp_path):
     assert r.returncode != 0
     assert r.stdout.count("Incorrect number of command line arguments specified") == 1, r.stdout
     assert not (tmp_path / "output").exists()
+
+
+@pytest.mark.gpu
+def test_mpirun_hip_rccl(heat3d_bin, tmp_path):
+    """The reference's exact GPU launch, ``mpirun -n P ./heat3D ...``
+    (heat3D.cu:203-205 MPI_Init, 650-654 cudaSetDevice), through the native
+    CLI with the HIP backend and RCCL: hydra's PMI_RANK / PMI_SIZE give the
+    rank, MPI_LOCALRANKID the device (local rank mod visible GPUs), the ranks
+    bootstrap the RCCL communicator over TCP.  One GPU here, so the launch is
+    MPMD with a per-rank NCCL_HOSTID (RCCL refuses two ranks of one host on
+    one device; as two "hosts" they talk over its socket transport on lo)."""
+    env = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_VARS}
+    env["HEAT3D_BOOTSTRAP_PORT"] = str(free_port())
+    env["HEAT3D_SHOW_PLACEMENT"] = "1"
+    args = ["33", "33", "33", "100000", "1e-5", "--backend", "hip", "--comm", "rccl", "--watchdog", "120"]
+    cmd = [MPIRUN, "-genv", "NCCL_SOCKET_IFNAME", "lo"]
+    for r in range(2):
+        if r:
+            cmd.append(":")
+        cmd += ["-n", "1", "-env", "NCCL_HOSTID", f"heat3d-mpirun-rank{r}", heat3d_bin] + args
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    out = r.stdout
+    assert out.count("Runnung HeatEquation3D with the following arguments:") == 1, out
+    assert "Simulation has converged in 3590 iterations with a convergence threshold of 1.000000e-05" in out
+    assert "L2-norm error: 0.0287 %" in out
+    assert "backend=hip comm=rccl ranks=2" in out, out
+    placed = sorted(l for l in r.stderr.splitlines() if l.startswith("heat3d: placement"))
+    assert len(placed) == 2, r.stderr[-3000:]
+    for rank, line in enumerate(placed):
+        m = re.search(r"rank=(\d+) size=2 local_rank=(\d+) from=MPI_LOCALRANKID device=(\d+) of (\d+)", line)
+        assert m, line
+        assert int(m.group(1)) == int(m.group(2)) == rank and int(m.group(3)) == rank % int(m.group(4)), line

@@ -323,3 +323,114 @@ def test_kernel_spec_z_stride_field(h3d):
     r = h3d.native().kernel_spec_resolved
     assert r("tl3:1:3:1:16:0:3:2:56", "fp64") == "tl3:1:3:1:16:0:3:2:56"
     assert r("tl3:2:3:1:16:0:3:2:112", "fp32") == "tl3:2:3:1:16:0:3:2:112"
+
+
+PREHEAT_CASES = [(1, (1, 1, 1)), (3, (3, 1, 1)), (8, (2, 2, 2))]
+
+
+@pytest.mark.parametrize("vr,dims", PREHEAT_CASES)
+@pytest.mark.parametrize("a_steps,b_steps", [(6, 9), (5, 7), (9, 12)])
+def test_preheat_is_state_neutral(h3d, vr, dims, a_steps, b_steps):
+    """Solver::preheat (bench.py's untimed warm-up right before the timed
+    window) rewrites nxt(cur()) with the next sweep's interior: step(a);
+    preheat(n); step(b) equals step(a + b) bit for bit in field, residual
+    and iteration count (single domain, x slabs on three buffers, 2x2x2)."""
+    n = (29, 27, 31)
+    mk = lambda: h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", virtual_ranks=vr, decomp=dims,
+                                extra_args=["--temporal", "3"])
+    a, b = mk(), mk()
+    assert a.native.temporal_blocking
+    if vr > 1:
+        assert a.native.field_buffers == 3
+    a.initialize(), b.initialize()
+    a.step(a_steps)
+    assert a.native.preheat(4) == 4 * vr
+    a.step(b_steps)
+    b.step(a_steps + b_steps)
+    a.synchronize(), b.synchronize()
+    sa, sb = a.native.state(), b.native.state()
+    assert sa["iter"] == sb["iter"] == a_steps + b_steps
+    assert sa["last_residual"] == sb["last_residual"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("vr,dims", PREHEAT_CASES)
+def test_preheat_keeps_rollback_input(h3d, vr, dims):
+    """A preheat issued after the converged sweep must not clobber that
+    sweep's input buffer, which the rollback recomputes the final field from
+    (with two buffers it is nxt(cur()) right after the sweep): the sweeps
+    honour the device done flag.  Converged iterations land at every offset
+    of a sweep; preheat right after the converged sweep and one sweep later."""
+    n = (25, 25, 25)
+    for eps in (1e-3, 9e-4, 8e-4):
+        extra = ["--temporal", "3", "--check-every", "6"]
+        ref = h3d.HeatSolver(n, 10 ** 6, eps, backend="cpu", virtual_ranks=vr, decomp=dims, extra_args=extra)
+        rr = ref.run()
+        assert rr["converged"]
+        c = rr["conv_iter"]
+        end = (c // 3 + 1) * 3  # first sweep boundary after the converged iteration
+        for extra_sweeps in (0, 1):
+            s = h3d.HeatSolver(n, 10 ** 6, eps, backend="cpu", virtual_ranks=vr, decomp=dims, extra_args=extra)
+            s.initialize()
+            s.step(end + 3 * extra_sweeps)
+            s.native.preheat(3)
+            r = s.run()
+            assert r["converged"] and r["conv_iter"] == c, (eps, r, c)
+            assert np.array_equal(s.gather(), ref.gather()), (vr, eps, extra_sweeps)
+
+
+LONG_HALO = [(3, (3, 1, 1)), (2, (2, 1, 1)), (4, (2, 2, 1)), (8, (2, 2, 2)), (3, (1, 1, 3))]
+
+
+@pytest.mark.parametrize("vr,dims", LONG_HALO)
+@pytest.mark.parametrize("K", [2, 3])
+def test_long_sweeps_across_halos(h3d, vr, dims, K):
+    """Step counts that are not multiples of K end in sweeps of depth K+1
+    across the halos (ghosts K+1 deep on split axes, exchanged K+1 deep
+    before a long sweep only) — the driver's 20-step window at N > 1 runs
+    4 x 3 + 2 x 4 instead of 6 x 3 + a partial 2 — bitwise equal to single
+    steps for every count, mixed with regular sweeps on the same fields."""
+    n = (33, 29, 31)
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", virtual_ranks=vr, decomp=dims,
+                       extra_args=["--temporal", str(K)])
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", extra_args=T1)
+    assert a.native.long_halo_sweeps
+    assert list(a.native.ghost_depth) == [K + 1 if d > 1 else 1 for d in dims]
+    a.initialize(), b.initialize()
+    for k in (5, 20, 7, 11, 4):
+        a.step(k)
+        b.step(k)
+        sa, sb = a.native.state(), b.native.state()
+        assert sa["iter"] == sb["iter"] and sa["last_residual"] == sb["last_residual"]
+        assert np.array_equal(a.gather(), b.gather()), (vr, dims, K, k)
+    assert a.native.verify_halos() == 0
+
+
+def test_long_sweeps_across_halos_off(h3d):
+    """--no-long-sweeps keeps K-deep ghosts (remainders as partial sweeps)."""
+    a = h3d.HeatSolver((33, 29, 31), 20, 0.0, backend="cpu", virtual_ranks=3, decomp=(3, 1, 1),
+                       extra_args=["--temporal", "3", "--no-long-sweeps"])
+    b = h3d.HeatSolver((33, 29, 31), 20, 0.0, backend="cpu", extra_args=T1)
+    assert not a.native.long_halo_sweeps and list(a.native.ghost_depth) == [3, 1, 1]
+    a.run(), b.run()
+    assert np.array_equal(a.gather(), b.gather())
+
+
+@pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (2, 2, 2))])
+def test_long_sweep_across_halos_rollback(h3d, vr, dims):
+    """Convergence inside a long (K+1) sweep across halos: the rollback
+    recomputes the final field from the sweep's input buffer, whose ghosts
+    that sweep exchanged K+1 deep."""
+    n = (25, 25, 25)
+    for eps in (1e-3, 9e-4, 8e-4, 7e-4):
+        ref = h3d.HeatSolver(n, 10 ** 6, eps, backend="cpu", extra_args=T1)
+        rr = ref.run()
+        c = rr["conv_iter"]
+        for j in (c // 3, c // 3 - 1):
+            s = h3d.HeatSolver(n, 10 ** 6, eps, backend="cpu", virtual_ranks=vr, decomp=dims,
+                               extra_args=["--temporal", "3"])
+            s.initialize()
+            s.step(3 * j + 8)  # 3 j steps in K-sweeps, then 2 long sweeps over c
+            r = s.run()
+            assert r["converged"] and r["conv_iter"] == c, (eps, j, r, c)
+            assert np.array_equal(s.gather(), ref.gather()), (vr, eps, j)

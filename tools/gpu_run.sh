@@ -19,6 +19,7 @@
 #   stats [BENCH ARGS]      rocprofv3 --kernel-trace --stats of bench.py    -> OUT/stats<i>/
 #   tune [TUNE ARGS]        python tools/tune.py ARGS                       -> OUT/tune<i>.log
 #   proxy [PROXY ARGS]      python tools/rank_proxy.py ARGS                 -> OUT/proxy<i>.json
+#   proxytrace [PROXY ARGS] the same under rocprofv3 --kernel-trace          -> OUT/proxytrace<i>/
 #   pmc VARIANT [N] [DTYPE] tools/pmc_passes.sh (one counter group per run) -> OUT/pmc<i>/
 #   py SCRIPT [ARGS]        any python script                              -> OUT/py<i>.log
 #   sh COMMAND...           a shell command (keep GPU work under its own timeout)
@@ -94,6 +95,11 @@ for step in "$@"; do
       timeout -k 10 400 python3 -u tools/rank_proxy.py "${args[@]}" > "$OUT/proxy$i.json" 2>&1 \
         || { rc=$?; tail -20 "$OUT/proxy$i.json"; fail proxy $rc; }
       tail -1 "$OUT/proxy$i.json" | cut -c1-300 ;;
+    proxytrace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$OUT/proxytrace$i" -o trace -- \
+        python3 -u tools/rank_proxy.py "${args[@]}" > "$OUT/proxytrace$i.log" 2>&1 \
+        || { rc=$?; tail -20 "$OUT/proxytrace$i.log"; fail proxytrace $rc; }
+      tail -1 "$OUT/proxytrace$i.log" | cut -c1-300 ;;
     pmc)
       bash tools/pmc_passes.sh "$OUT/pmc$i" "${args[@]}" || fail pmc $?
       echo "pmc done" ;;

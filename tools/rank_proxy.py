@@ -37,8 +37,11 @@ def main() -> int:
     ap.add_argument("--ar-us", type=float, default=20.0, help="emulated all-reduce latency (us)")
     ap.add_argument("--backend", default="hip")
     ap.add_argument("--extra", default="", help="extra solver flags, e.g. '--no-overlap'")
+    ap.add_argument("--preheat-ms", type=float, default=0.0,
+                    help="as bench.py --preheat-ms: untimed idempotent sweeps right before the timed window "
+                         "(the driver-config rehearsal: --steps 20 --warmup 5 --preheat-ms 20)")
     ap.add_argument("--trace-schedule", action="store_true",
-                    help="print the start-up schedule tuner's candidate timings (HEAT3D_TRACE during initialize)")
+                    help="print the start-up schedule tuner's candidate timings (HEAT3D_TRACE, read once: on for the whole run)")
     args = ap.parse_args()
 
     import heat3d_amd
@@ -63,7 +66,14 @@ def main() -> int:
     os.environ.pop("HEAT3D_TRACE", None)
     free_after, total = s.native.mem_info()
     s.step(args.warmup)
+    s.prepare_steps(args.steps)
     s.synchronize()
+    preheat = 0
+    if args.preheat_ms > 0:
+        K = s.native.temporal_steps
+        est_ms = s.interior_points / P * max(1, K) / (800e9 if args.dtype == "fp64" else 1400e9) * 1e3
+        preheat = s.native.preheat(max(1, min(64, int(args.preheat_ms / max(est_ms, 1e-3)) + 1)))
+        s.synchronize()
     t0 = time.perf_counter()
     s.step(args.steps)
     s.synchronize()
@@ -74,6 +84,7 @@ def main() -> int:
     phases = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in s.native.profile_sweeps(8).items()}
     out = {"proxy": "phantom rank", "rank": r, "ranks": P, "dims": list(dims), "grid": args.grid,
            "dtype": args.dtype, "gbps": args.gbps, "ar_us": args.ar_us, "extra": args.extra,
+           "steps": args.steps, "warmup": args.warmup, "preheat_sweeps": preheat,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "kernel": s.kernel,
            "reserved_cus": s.native.reserved_cus, "graph_launches": s.native.graph_launches,
            "projected_node_glups": round(s.interior_points * args.steps / dt / 1e9, 2),
