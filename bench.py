@@ -279,8 +279,13 @@ def run_rank(args) -> int:
     # the x schedules timed at start-up (Config autotune): L = -3 is the
     # dispatch model's plan, L > 0 fixed x segments of L planes
     xs = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in t.items()} for t in ext.tuned_schedules()]
+    # remainder policy (Solver::calibrate_remainders): which n mod K end in
+    # K+1-step sweeps, from the start-up sweep timings (ms)
     placement = all_gather_objects({"rank": rank, "device": dev, "host": socket.gethostname(),
-                                    "subdomain": list(s.native.local_subdomain(0)["n"]), "x_schedules": xs}, group)
+                                    "subdomain": list(s.native.local_subdomain(0)["n"]), "x_schedules": xs,
+                                    "long_remainders": list(s.native.long_remainders),
+                                    "sweep_costs_ms": {k: round(v, 4) for k, v in s.native.sweep_costs.items()}},
+                                   group)
     # per-rank schedule profile, after (outside) the timed window: a few more
     # sweeps of the same pipeline with timing events at its phase boundaries
     # (interior / halo / boundary / all-reduce / check, compute-stream idle,

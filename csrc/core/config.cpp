@@ -113,6 +113,8 @@ std::string Config::usage() {
      << "  --lag auto|on|off         lagged convergence check of overlapped sweeps (3rd field buffer)\n"
      << "  --no-block-overlap        block decompositions: exchange the halo first, then sweep\n"
      << "  --no-long-sweeps          step-count remainders as partial sweeps, not K+1-step sweeps\n"
+     << "  --long-sweeps auto|on|off remainders as K+1-step sweeps: auto = where the start-up timing of\n"
+     << "                            the sweeps finds them cheaper than a partial sweep (default auto)\n"
      << "  --autotune auto|on|off    time the sweep schedule candidates (z stride, x segments) at start-up;\n"
      << "                            auto: single-subdomain runs (--no-autotune = off)\n"
      << "  --graph-multistream       record the overlapped multi-stream schedule into hipGraphs too\n"
@@ -230,7 +232,14 @@ Config Config::parse(int argc, const char* const* argv) {
       else throw UsageError("--lag must be auto, on or off");
     }
     else if (key == "--no-block-overlap") c.block_overlap = false;
-    else if (key == "--no-long-sweeps") c.long_sweeps = false;
+    else if (key == "--no-long-sweeps") c.long_sweeps = 0;
+    else if (key == "--long-sweeps") {
+      const std::string v = get("--long-sweeps");
+      if (v == "auto") c.long_sweeps = -1;
+      else if (v == "on") c.long_sweeps = 1;
+      else if (v == "off") c.long_sweeps = 0;
+      else throw UsageError("--long-sweeps takes auto, on or off");
+    }
     else if (key == "--no-autotune") c.autotune = 0;
     else if (key == "--autotune") {
       const std::string v = get("--autotune");

@@ -74,7 +74,9 @@ struct Config {
   // --- schedule / runtime knobs (until round 2 HEAT3D_* environment variables)
   int lag = -1;                   // lagged convergence check of overlapped sweeps (third buffer): -1 auto, 0 off, 1 on
   bool block_overlap = true;      // block decompositions: interior || halo (false: exchange first)
-  bool long_sweeps = true;        // K+1-step sweeps absorb step counts that are not multiples of K
+  // K+1-step sweeps absorb step counts that are not multiples of K: -1 auto
+  // (GPU: where timed at start-up cheaper than the partial sweep), 1 always, 0 never
+  int long_sweeps = -1;
   // time the interior sweeps' schedule candidates at initialisation: -1 auto
   // (single-subdomain runs, whose sweeps run alone as they are timed), 0 off, 1 on
   int autotune = -1;

@@ -622,6 +622,11 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
   H3D_TBLA(3, 16, 3, 18, false) H3D_TBLA(3, 16, 3, 19, false)
   H3D_TBLA(2, 16, 4, 2, false) H3D_TBLA(3, 16, 2, 2, false)
   H3D_TBLA(3, 12, 4, 2, true)  // the fp64 K = 4 default (long sweeps: 12 waves, 36 rows)
+  // deeper T^n prefetch with nt stores (Q = 6: plane x+4 loaded at step x)
+  if (R == 3 && WY == 16 && K == 3 && Q == 6 && r.O == 2) {
+    if (p) launch_tbl<Real, 3, 16, 3, 6, 2>(*p, k, s);
+    return true;
+  }
   H3D_TBLA(4, 12, 4, 2, false)
 #undef H3D_TBLA
   // 16 waves (<= 128 VGPRs, LDS 2K x 16 KiB): K <= 4; 12 waves (<= 168 VGPRs): K = 5

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
                                                        TBPArgs g, float Dxs, float Dys, float Dzs,
                                                        unsigned long long* res, const int* done) {
   static_assert(K >= 2 && K <= 6, "temporal depth");
-  static_assert(Q == 3 || Q == 4, "T^n ring size");
+  static_assert(Q == 3 || Q == 4 || Q == 6, "T^n ring size");
   constexpr int TY = WY * R;
   constexpr int YS = TY - 2 * K;       // tile stride along y (stored rows)
   constexpr int U = lcm_p(lcm_p(Q, 3), 2);
@@ -473,6 +473,12 @@ static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) 
   }
   H3D_TBPA(2) H3D_TBPA(3) H3D_TBPA(17) H3D_TBPA(19)
 #undef H3D_TBPA
+  // Q = 6: plane x+4 loaded at step x (3 steps of latency cover), nt stores
+  if (R == 3 && WY == 16 && K == 3 && Q == 6 && r.O == 2) {
+    if (p) launch_tbp<3, 16, 3, 6, 2>(*p, k, s);
+    return true;
+  }
+  H3D_TBP(3, 16, 3, 6) H3D_TBP(2, 16, 3, 6)
   H3D_TBP(3, 16, 3, 3) H3D_TBP(3, 16, 3, 4) H3D_TBP(2, 16, 3, 3) H3D_TBP(2, 16, 4, 3) H3D_TBP(2, 16, 4, 4)
   H3D_TBP(3, 16, 4, 3) H3D_TBP(2, 16, 2, 3) H3D_TBP(3, 16, 2, 3)
 #undef H3D_TBP

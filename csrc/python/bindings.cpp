@@ -715,6 +715,19 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("field_buffers", &Solver::field_buffers)
       .def_property_readonly("ghost_depth", &Solver::ghost_depth)
       .def_property_readonly("long_halo_sweeps", &Solver::long_halo_sweeps)
+      .def_property_readonly("long_remainders",
+                             [](const Solver& s) {
+                               std::vector<int> r;
+                               for (int i = 1; i < s.temporal_steps(); ++i)
+                                 if ((s.long_remainders() >> i) & 1u) r.push_back(i);
+                               return r;
+                             })
+      .def_property_readonly("sweep_costs",
+                             [](const Solver& s) {
+                               py::dict d;
+                               for (auto& kv : s.sweep_costs()) d[py::str(kv.first)] = kv.second;
+                               return d;
+                             })
       .def_property_readonly("backend_name", [](Solver& s) { return std::string(s.backend().name()); })
       .def_property_readonly("comm_name", [](Solver& s) { return std::string(s.comm().name()); })
       .def_property_readonly("comm_size", [](Solver& s) { return s.comm().size(); })

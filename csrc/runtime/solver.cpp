@@ -491,6 +491,7 @@ void Solver::initialize() {
     }
   }
   tune_schedules();
+  calibrate_remainders();
   DeviceState hs;
   std::memset(&hs, 0, sizeof(hs));
   for (auto& r : hs.residual) r = kResidualInitBits;
@@ -568,6 +569,90 @@ void Solver::tune_schedules() {
     }
   }
   be_->sync(kCompute);
+}
+
+// Remainder policy.  A step count n = a K + r (0 < r < K) either ends in a
+// partial sweep of r steps (r = 1: a single step) or runs r of its sweeps as
+// long sweeps of K+1 steps: long costs r (T_{K+1} - T_K) more sweep time,
+// partial costs T_r.  Which is cheaper depends on the box: on one GPU's
+// 1022^3 a K = 2 sweep takes 95% of a K = 3 one (3.5 vs 3.7 ms; long wins),
+// on the 8-GPU slab share's 122-plane interior the K = 4 sweep takes 1.73x
+// the K = 3 one (936 vs 540 us: its 36-row tiles need 2.8 rounds of
+// workgroups against 1.8) while K = 2 takes 0.96x (partial wins).  So each
+// rank times its interior sweeps once at start-up (idempotent sweeps into
+// the next buffer, no residual state, as tune_schedules) and the ranks agree
+// by vote: long for remainder r only where every rank found it cheaper.
+void Solver::calibrate_remainders() {
+  long_rem_ = ~0u;
+  sweep_costs_.clear();
+  if (!tb_ || cfg_.long_sweeps == 0) {
+    long_rem_ = 0;
+    return;
+  }
+  if (cfg_.long_sweeps > 0 || !be_->is_gpu() || (has_halo_ && !long_halo_) || K_ + 1 > 6) return;
+  {
+    KernelSpec kl;
+    kl.kind = kspec2_.kind;
+    kl.K = K_ + 1;
+    if (!hip::lean_supported(dt_, kl)) return;
+  }
+  Event e0 = be_->event_create(), e1 = be_->event_create();
+  // Kp = 1: a single step of the owned box; else a sweep of depth Kp
+  auto launch = [&](int Kp) {
+    for (auto& l : local_) {
+      StencilParams sp;
+      sp.in = l.field[0];
+      sp.out = l.field[nxt(0)];
+      sp.L = l.L;
+      for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+      sp.state = nullptr;
+      sp.cu_reserved = be_->reserved_cus();
+      if (Kp == 1) {
+        sp.box = l.owned;
+        be_->stencil(dt_, sp, kspec_, kCompute);
+        continue;
+      }
+      sp.box = Kp > K_ ? l.tb_interior_long : l.tb_interior;
+      if (sp.box.empty()) continue;
+      auto shrink = [&](const int64_t (&u)[2], int64_t nn, int64_t (&o)[2]) {
+        o[0] = u[0] < 0 ? -(Kp - 1) : u[0];
+        o[1] = u[1] > nn ? nn + Kp - 1 : u[1];
+      };
+      shrink(l.ux, l.sd.n[0], sp.ux);
+      shrink(l.uy, l.sd.n[1], sp.uy);
+      shrink(l.uz, l.sd.n[2], sp.uz);
+      KernelSpec ks = kspec2_;
+      if (Kp != K_) {
+        ks = KernelSpec();
+        ks.kind = kspec2_.kind;
+        ks.K = Kp;
+      }
+      be_->sweep(dt_, sp, ks, kCompute);
+    }
+  };
+  auto cost = [&](int Kp) {
+    launch(Kp);  // warm (code object, caches)
+    constexpr int reps = 3;
+    be_->record(e0, kCompute);
+    for (int i = 0; i < reps; ++i) launch(Kp);
+    be_->record(e1, kCompute);
+    be_->sync(kCompute);
+    const double ms = be_->elapsed_ms(e0, e1) / reps;
+    sweep_costs_.push_back({Kp == 1 ? std::string("step") : "sweep" + std::to_string(Kp), ms});
+    return ms;
+  };
+  const double tk = cost(K_), tl = cost(K_ + 1);
+  unsigned long long votes = 0;
+  for (int r = 1; r < K_; ++r)
+    if (r * (tl - tk) < cost(r)) votes |= 1ull << (12 * r);
+  be_->event_destroy(e0);
+  be_->event_destroy(e1);
+  const unsigned long long voters = comm_->all_local() || comm_->size() == 1 ? 1 : (unsigned long long)comm_->size();
+  votes = allreduce_sum_u64(votes);
+  long_rem_ = 0;
+  for (int r = 1; r < K_; ++r)
+    if (((votes >> (12 * r)) & 0xfff) == voters) long_rem_ |= 1u << r;
+  be_->sync_all();
 }
 
 int Solver::preheat(int sweeps) {
@@ -1097,7 +1182,7 @@ int Solver::long_sweeps_for(int64_t n) const {
   if (K_ + 1 > 6 || K_ + 1 > kResidualSlots) return 0;
   const int64_t b = n % K_;             // n = a K + b (K + 1) with a = (n - b (K + 1)) / K
   if (b * (K_ + 1) > n) return 0;
-  if (!cfg_.long_sweeps) return 0;
+  if (!cfg_.long_sweeps || !((long_rem_ >> b) & 1u)) return 0;
   // the K+1 variant must exist for this dtype (e.g. fp64 K = 5 has no K = 6)
   KernelSpec ks;
   ks.kind = kspec2_.kind;

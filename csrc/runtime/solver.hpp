@@ -130,6 +130,10 @@ class Solver {
   // long sweeps cross the halos) and whether they do
   std::array<int64_t, 3> ghost_depth() const { return {hd_[0], hd_[1], hd_[2]}; }
   bool long_halo_sweeps() const { return long_halo_; }
+  // remainder policy: which n mod K run as long sweeps, and the start-up
+  // sweep timings that decided it (empty when not measured)
+  unsigned long_remainders() const { return long_rem_; }
+  const std::vector<std::pair<std::string, double>>& sweep_costs() const { return sweep_costs_; }
   // HBM preflight (constructor): bytes this solver allocates for its local
   // ranks (fields + face staging), and the backend's free / total memory
   // just before those allocations (0 when the backend cannot tell)
@@ -279,6 +283,11 @@ class Solver {
   // not multiples of K end in long sweeps instead of a partial K-1 sweep
   bool long_halo_ = false;
   int slot_stride_ = 1;       // residual slots per sweep bank of the lagged schedule
+  // remainder policy (long_sweeps_for): bit r set = a step count with n mod K
+  // = r ends in r long sweeps, else in a partial sweep of r steps
+  unsigned long_rem_ = ~0u;
+  std::vector<std::pair<std::string, double>> sweep_costs_;  // start-up timings (ms per sweep)
+  void calibrate_remainders();
   int last_bnd_ = 0;          // boundary-layer depth of the last overlapped sweep (0: none pending)
   bool ordered_halo_ = false; // axis-ordered exchange filling edges / corners (deep y / z halos)
   int last_kind_ = 0;         // 1 = single step, 2 = pair: last enqueued schedule

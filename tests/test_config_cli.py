@@ -156,3 +156,21 @@ def test_schedule_flags(heat3d_bin, tmp_path):
     assert bad.returncode != 0 and "--autotune auto|on|off" in (bad.stdout + bad.stderr)
     h = run_cli(["--help"], tmp_path)
     assert "--autotune auto|on|off" in h.stdout + h.stderr
+
+
+def test_progress_heartbeat(heat3d_bin, tmp_path):
+    """--progress S: run() prints a heartbeat to stderr (iteration, relative
+    residual, eps, elapsed, GLUPS) at most every S seconds, so that long
+    convergence runs stay visibly alive; stdout keeps the reference report."""
+    r = run_cli(["33", "33", "33", "100000", "1e-5", "--backend", "cpu", "--output", "none",
+                 "--progress", "0.001", "--check-every", "64"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    beats = [l for l in r.stderr.splitlines() if l.startswith("heat3d: progress iteration")]
+    assert beats, r.stderr[-2000:]
+    its = [int(l.split()[3]) for l in beats]
+    assert its == sorted(its) and its[-1] <= 3591
+    assert "relative" in beats[0] and "(eps 1.000e-05)" in beats[0]
+    assert "heat3d: progress" not in r.stdout
+    assert "Simulation has converged in 3590 iterations" in r.stdout
+    bad = run_cli(["33", "33", "33", "10", "1e-5", "--backend", "cpu", "--progress", "-1"], tmp_path)
+    assert bad.returncode != 0

@@ -503,7 +503,8 @@ def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype):
     long K+1 sweeps across the halos, including the (K+1)-plane boundary
     slabs (y-marching K = 4 thin-slab tiles), bitwise equal to single steps."""
     n = (82, 70, 150)
-    a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims)
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims,
+                       extra_args=["--long-sweeps", "on"])
     b = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
     assert a.native.long_halo_sweeps
     a.initialize(), b.initialize()
@@ -525,9 +526,33 @@ def test_long_sweep_across_halos_rollback_gpu(h3d, gpu, vr, dims):
         rr = ref.run()
         c = rr["conv_iter"]
         for j in (c // 3, c // 3 - 1):
-            s = h3d.HeatSolver(n, 10 ** 6, eps, backend="hip", virtual_ranks=vr, decomp=dims)
+            s = h3d.HeatSolver(n, 10 ** 6, eps, backend="hip", virtual_ranks=vr, decomp=dims,
+                               extra_args=["--long-sweeps", "on"])
             s.initialize()
             s.step(3 * j + 8)
             r = s.run()
             assert r["converged"] and r["conv_iter"] == c, (eps, j, r, c)
             assert np.array_equal(s.gather(), ref.gather()), (vr, eps, j)
+
+
+@pytest.mark.parametrize("vr,dims", [(1, (1, 1, 1)), (3, (3, 1, 1))])
+def test_remainder_policy_measured_gpu(h3d, gpu, vr, dims):
+    """--long-sweeps auto (default): the start-up timing of the K, K+1 and
+    partial sweeps picks, per remainder, long sweeps or a partial one; either
+    way the result equals single steps bit for bit."""
+    n = (82, 70, 150)
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="hip", virtual_ranks=vr, decomp=dims)
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="hip", extra_args=["--temporal", "1"])
+    a.initialize(), b.initialize()
+    costs = a.native.sweep_costs
+    assert set(costs) == {"sweep3", "sweep4", "step", "sweep2"} and all(v > 0 for v in costs.values()), costs
+    rem = a.native.long_remainders
+    for r in (1, 2):
+        assert (r in rem) == (r * (costs["sweep4"] - costs["sweep3"]) < costs["step" if r == 1 else "sweep2"]), \
+            (rem, costs)
+    for k in (5, 20, 7):
+        a.step(k)
+        b.step(k)
+    a.synchronize(), b.synchronize()
+    assert a.native.state()["iter"] == b.native.state()["iter"] == 32
+    assert np.array_equal(a.gather(), b.gather())
