@@ -61,8 +61,13 @@ def parse_args(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph-chunk", type=int, default=32)
-    ap.add_argument("--converge-eps", type=float, default=1e-3,
-                    help="also measure time-to-converge at this EPS (0 disables)")
+    ap.add_argument("--converge-eps", type=float, default=1e-5,
+                    help="also measure time-to-converge at this EPS (0 disables).  Default: the reference's "
+                         "tolerance 1e-5 (1024^3 fp64: 186188 iterations, 240 s on one MI355X, 21.5%% off the "
+                         "steady state; profiles/converge_1024_r04.md)")
+    ap.add_argument("--converge-time-limit", type=float, default=360.0,
+                    help="wall budget (s) of the time-to-converge run: past it the run stops unconverged and "
+                         "the JSON says so (bounds the driver's bench on a slow box; 0 = none)")
     ap.add_argument("--temporal", type=int, default=0, help="0 auto | 1 single-step | K (2..6) K-step temporally blocked sweeps")
     ap.add_argument("--kernel2", default="auto", help="temporally blocked sweep kernel (tbK / trK[:V:R:WZ:WY:L:Q])")
     ap.add_argument("--virtual-ranks", type=int, default=1,
@@ -300,13 +305,16 @@ def run_rank(args) -> int:
     ttc = None
     if args.converge_eps and args.converge_eps > 0:
         c = make(args.converge_eps, 10 ** 7,
-                 ["--progress", str(args.progress)] + (["--verbose", str(args.verbose)] if args.verbose > 0 else []))
+                 ["--progress", str(args.progress), "--time-limit", str(args.converge_time_limit)]
+                 + (["--verbose", str(args.verbose)] if args.verbose > 0 else []))
         c.initialize()
         barrier(group)
         r = c.run()
         ttc = {"eps": args.converge_eps, "converged": bool(r["converged"]),
-               "iterations": int(r["conv_iter"]), "seconds": max_over_ranks(r["seconds"], group),
-               "error_percent": r["error_percent"]}
+               "iterations": int(r["conv_iter"]) if r["converged"] else int(r["iterations"]),
+               "seconds": max_over_ranks(r["seconds"], group),
+               "error_percent": r["error_percent"], "time_limit_s": args.converge_time_limit,
+               "relative_residual": r["last_residual"] / r["norm"] if r["norm"] else None}
         del c
 
     par = "x".join(str(d) for d in dims)

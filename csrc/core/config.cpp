@@ -106,6 +106,7 @@ std::string Config::usage() {
      << "  --timers                  per-phase GPU timing (synchronised diagnostic run)\n"
      << "  --verbose N               print residual every N iterations\n"
      << "  --progress S              stderr heartbeat (iteration, residual, rate) every S seconds of run()\n"
+     << "  --time-limit S            run(): stop (not converged) after about S seconds (0 = no limit)\n"
      << "  --threads N               CPU backend OpenMP threads\n"
      << "  --reserve-cus N           CUs kept free of the interior sweep for comm / boundary / check\n"
      << "                            kernels (default: 8 = one per XCD when the overlapped\n"
@@ -221,6 +222,7 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--json-out") c.json_out = get("--json-out");
     else if (key == "--verbose") c.verbose = (int)to_i64(get("--verbose"), "--verbose");
     else if (key == "--progress") c.progress_s = to_f64(get("--progress"), "--progress");
+    else if (key == "--time-limit") c.time_limit_s = to_f64(get("--time-limit"), "--time-limit");
     else if (key == "--threads") c.cpu_threads = (int)to_i64(get("--threads"), "--threads");
     else if (key == "--reserve-cus") c.reserve_cus = (int)to_i64(get("--reserve-cus"), "--reserve-cus");
     else if (key == "--quiet") c.quiet = true;
@@ -288,6 +290,7 @@ Config Config::parse(int argc, const char* const* argv) {
   if (c.io_stage_mb < 1) c.io_stage_mb = 1;
   if (c.watchdog_s <= 0) throw UsageError("--watchdog must be > 0");
   if (c.progress_s < 0) throw UsageError("--progress must be >= 0");
+  if (c.time_limit_s < 0) throw UsageError("--time-limit must be >= 0");
   return c;
 }
 

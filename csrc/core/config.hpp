@@ -67,6 +67,7 @@ struct Config {
   std::string json_out;
   int verbose = 0;
   double progress_s = 0;          // run(): stderr heartbeat period (0 = off)
+  double time_limit_s = 0;        // run(): wall budget, stop unconverged past it (0 = none)
   bool quiet = false;
   int cpu_threads = 0;
   int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules

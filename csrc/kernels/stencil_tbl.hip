@@ -58,6 +58,7 @@ struct TBLArgs {
   int nzb, nyb;
   int segsplit, n1, rb;        // x plan: seg | split << 16, whole pieces, r | split-tail << 30
   int zs;                      // tile stride along z = stored columns per tile (<= 64 - 2K)
+  int tord;                    // tile order (tile_coords)
 };
 
 namespace {
@@ -179,7 +180,8 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
   const int xlo_p = (int)(w - (int64_t)tt * nxb);
   const int xhi_p = (int)min((int64_t)nxb, xlo_p + (wend - w));
   w += xhi_p - xlo_p;
-  const int zb = tt % g.nzb, ybk = tt / g.nzb;
+  int zb, ybk;
+  tile_coords(tt, g.nzb, g.nyb, g.tord, zb, ybk);
 
   const int wave = sgpr(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -438,6 +440,7 @@ static void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t
                    Lsy * (int64_t)sizeof(Real) * (R + 2 * Lg1 + TY + 2 * K) < (1LL << 31),
                "tl: extents exceed 32-bit tile coordinates");
   TBLArgs g;
+  g.tord = tile_order();
   g.sx = Lsx;
   g.sy = Lsy;
   g.origin = L.origin;
@@ -622,11 +625,6 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
   H3D_TBLA(3, 16, 3, 18, false) H3D_TBLA(3, 16, 3, 19, false)
   H3D_TBLA(2, 16, 4, 2, false) H3D_TBLA(3, 16, 2, 2, false)
   H3D_TBLA(3, 12, 4, 2, true)  // the fp64 K = 4 default (long sweeps: 12 waves, 36 rows)
-  // deeper T^n prefetch with nt stores (Q = 6: plane x+4 loaded at step x)
-  if (R == 3 && WY == 16 && K == 3 && Q == 6 && r.O == 2) {
-    if (p) launch_tbl<Real, 3, 16, 3, 6, 2>(*p, k, s);
-    return true;
-  }
   H3D_TBLA(4, 12, 4, 2, false)
 #undef H3D_TBLA
   // 16 waves (<= 128 VGPRs, LDS 2K x 16 KiB): K <= 4; 12 waves (<= 168 VGPRs): K = 5

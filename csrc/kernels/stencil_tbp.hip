@@ -51,6 +51,7 @@ struct TBPArgs {
   int segsplit, n1, rb;        // x plan (TBRArgs encoding)
   int hl;                      // first stored column of a tile, from its first loaded one
   int zs;                      // tile stride along z = stored columns per tile (even, <= 128 - 2K - 2)
+  int tord;                    // tile order (tile_coords)
 };
 
 namespace {
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
                                                        TBPArgs g, float Dxs, float Dys, float Dzs,
                                                        unsigned long long* res, const int* done) {
   static_assert(K >= 2 && K <= 6, "temporal depth");
-  static_assert(Q == 3 || Q == 4 || Q == 6, "T^n ring size");
+  static_assert(Q == 3 || Q == 4, "T^n ring size");
   constexpr int TY = WY * R;
   constexpr int YS = TY - 2 * K;       // tile stride along y (stored rows)
   constexpr int U = lcm_p(lcm_p(Q, 3), 2);
@@ -130,10 +131,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
     pc = g.n1 + remap(blk - g.n1 - rr, rr);
     part = 2;
   }
-  const int zb = pc % g.nzb;
-  const int tq = pc / g.nzb;
-  const int ybk = tq % g.nyb;
-  const int xs = tq / g.nyb;
+  const int ntile = g.nzb * g.nyb;
+  const int xs = pc / ntile;
+  int zb, ybk;
+  tile_coords(pc - xs * ntile, g.nzb, g.nyb, g.tord, zb, ybk);
   const int nxb = g.bhi[0] - g.blo[0];
   const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
   int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
@@ -359,6 +360,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
                    L.sy * (int64_t)sizeof(float) * (R + 2 * L.gy + TY + 2 * K) < (1LL << 31),
                "tl pair: extents exceed 32-bit tile coordinates");
   TBPArgs g;
+  g.tord = tile_order();
   g.sx = L.sx;
   g.sy = L.sy;
   g.origin = L.origin;
@@ -473,12 +475,7 @@ static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) 
   }
   H3D_TBPA(2) H3D_TBPA(3) H3D_TBPA(17) H3D_TBPA(19)
 #undef H3D_TBPA
-  // Q = 6: plane x+4 loaded at step x (3 steps of latency cover), nt stores
-  if (R == 3 && WY == 16 && K == 3 && Q == 6 && r.O == 2) {
-    if (p) launch_tbp<3, 16, 3, 6, 2>(*p, k, s);
-    return true;
-  }
-  H3D_TBP(3, 16, 3, 6) H3D_TBP(2, 16, 3, 6)
+
   H3D_TBP(3, 16, 3, 3) H3D_TBP(3, 16, 3, 4) H3D_TBP(2, 16, 3, 3) H3D_TBP(2, 16, 4, 3) H3D_TBP(2, 16, 4, 4)
   H3D_TBP(3, 16, 4, 3) H3D_TBP(2, 16, 2, 3) H3D_TBP(3, 16, 2, 3)
 #undef H3D_TBP

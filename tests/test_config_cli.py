@@ -174,3 +174,20 @@ def test_progress_heartbeat(heat3d_bin, tmp_path):
     assert "Simulation has converged in 3590 iterations" in r.stdout
     bad = run_cli(["33", "33", "33", "10", "1e-5", "--backend", "cpu", "--progress", "-1"], tmp_path)
     assert bad.returncode != 0
+
+
+@pytest.mark.parametrize("gpus", [1, 3])
+def test_time_limit(heat3d_bin, tmp_path, gpus):
+    """--time-limit S: run() stops unconverged after about S seconds; the
+    wall budget becomes one iteration cap agreed by every rank (min over the
+    ranks' projections, one all-reduce), so the ranks stop at the same
+    iteration and the job exits cleanly (3 ranks: socket transport)."""
+    args = ["65", "65", "65", "100000000", "1e-12", "--backend", "cpu", "--output", "none", "--threads", "2",
+            "--time-limit", "2", "--check-every", "16", "--json-out", "t.json"]
+    if gpus > 1:
+        args += ["--gpus", str(gpus)]
+    r = run_cli(args, tmp_path, env={"HEAT3D_BOOTSTRAP_PORT": str(free_port())})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Simulation did not converge" in r.stdout
+    j = json.loads((tmp_path / "t.json").read_text())
+    assert not j["converged"] and 0 < j["seconds"] < 6, j
