@@ -39,33 +39,6 @@ __device__ __forceinline__ Real ftcs(Real c, Real xm, Real xp, Real ym, Real yp,
 // ---- cross-lane helpers ----------------------------------------------------
 // DPP wave_shr:1 (0x138): lane i <- lane i-1 ; lane 0 keeps `old`.
 // DPP wave_shl:1 (0x130): lane i <- lane i+1 ; lane 63 keeps `old`.
-// Tile index -> (z, y) tile coordinates of the sweep kernels.  ord = 0:
-// row-major (z fastest).  ord = BY << 8 | BZ: blocks of BY x BZ tiles (z
-// fastest inside a block, blocks row-major, narrower blocks at the z end and
-// a shorter block-row at the y end), so that the consecutive pieces one XCD
-// runs at once form a compact 2D patch: more of the halo rows and columns
-// the tiles share are read while a neighbour's copy is still in that XCD's L2.
-__device__ __forceinline__ void tile_coords(int t, int nzb, int nyb, int ord, int& zb, int& yb) {
-  if (ord == 0) {
-    zb = t % nzb;
-    yb = t / nzb;
-    return;
-  }
-  const int BZ = ord & 0xff, BY = ord >> 8;
-  const int R = t / (BY * nzb), rem = t - R * BY * nzb;
-  const int by = min(BY, nyb - R * BY);
-  const int f = nzb / BZ;  // full-width block columns
-  if (rem < f * by * BZ) {
-    const int C = rem / (by * BZ), r2 = rem - C * by * BZ;
-    zb = C * BZ + r2 % BZ;
-    yb = R * BY + r2 / BZ;
-  } else {
-    const int w = nzb - f * BZ, r2 = rem - f * by * BZ;
-    zb = f * BZ + r2 % w;
-    yb = R * BY + r2 / w;
-  }
-}
-
 __device__ __forceinline__ double dpp_shr1(double old, double v) {
   long long ov = __builtin_bit_cast(long long, old), vv = __builtin_bit_cast(long long, v);
   int lo = __builtin_amdgcn_update_dpp((int)ov, (int)vv, 0x138, 0xf, 0xf, false);
@@ -191,9 +164,6 @@ struct XPlan {
 // to chunks of U); cached per shape.  equal_only: no split (previous policy).
 // HEAT3D_TRACE launch diagnostics (read once per process)
 bool trace_enabled();
-// tile order of the sweep kernels (tile_coords): HEAT3D_TILE_ORDER=BYxBZ, read
-// once per process; 0 = row-major
-int tile_order();
 XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_only = false);
 XPlan fixed_xplan(int64_t nx, int64_t tiles, int seg);
 // Makespan of a plan in the same greedy-dispatch model (plane steps per slot).

@@ -244,16 +244,6 @@ bool trace_enabled() {
   return on;
 }
 
-int tile_order() {
-  static const int ord = [] {
-    const char* e = std::getenv("HEAT3D_TILE_ORDER");
-    int by = 0, bz = 0;
-    if (!e || std::sscanf(e, "%dx%d", &by, &bz) != 2 || by < 1 || bz < 1 || by > 255 || bz > 255) return 0;
-    return by << 8 | bz;
-  }();
-  return ord;
-}
-
 int device_cus() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -51,7 +51,6 @@ struct TBPArgs {
   int segsplit, n1, rb;        // x plan (TBRArgs encoding)
   int hl;                      // first stored column of a tile, from its first loaded one
   int zs;                      // tile stride along z = stored columns per tile (even, <= 128 - 2K - 2)
-  int tord;                    // tile order (tile_coords)
 };
 
 namespace {
@@ -131,10 +130,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
     pc = g.n1 + remap(blk - g.n1 - rr, rr);
     part = 2;
   }
-  const int ntile = g.nzb * g.nyb;
-  const int xs = pc / ntile;
-  int zb, ybk;
-  tile_coords(pc - xs * ntile, g.nzb, g.nyb, g.tord, zb, ybk);
+  const int zb = pc % g.nzb;
+  const int tq = pc / g.nzb;
+  const int ybk = tq % g.nyb;
+  const int xs = tq / g.nyb;
   const int nxb = g.bhi[0] - g.blo[0];
   const int seg = g.segsplit & 0xffff, split = g.segsplit >> 16;
   int xlo_p = xs * seg, xhi_p = min(xlo_p + seg, nxb);
@@ -360,7 +359,6 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
                    L.sy * (int64_t)sizeof(float) * (R + 2 * L.gy + TY + 2 * K) < (1LL << 31),
                "tl pair: extents exceed 32-bit tile coordinates");
   TBPArgs g;
-  g.tord = tile_order();
   g.sx = L.sx;
   g.sy = L.sy;
   g.origin = L.origin;

@@ -113,6 +113,14 @@ KernelSpec KernelSpec::resolved(DType t) const {
         r.R = 3;
         r.WY = 12;
       }
+      // fp64 K = 2 (partial sweeps of multi-rank step-count remainders): 16
+      // waves of 5 rows (80-row tiles, 114 VGPRs), nt stores.  Fewer y-halo
+      // rows per stored one than 48-row tiles: +7-11% at kernel level on the
+      // 1022^3, 508 / 250 / 122-plane slab boxes (profiles/probes_r04.md)
+      if (f64 && K == 2 && r.V == 1 && r.R == 0 && r.WY == 0) {
+        r.R = 5;
+        r.WY = 16;
+      }
       // fp64 K = 5 / 6 and fp32 K = 6: no 16-wave shape fits 128 VGPRs
       // without spilling; 8 waves of 3 rows (24-row tiles, up to 256 VGPRs)
       if ((f64 ? K >= 5 : K >= 6) && r.V == 1 && r.R == 0 && r.WY == 0) {
@@ -137,7 +145,7 @@ KernelSpec KernelSpec::resolved(DType t) const {
       if (!f64 && r.O < 0 && r.V == 2 && K == 3 && r.R == 3 && r.WY == 16 && r.NT == 3) r.O = 2;
       if (f64 && r.O < 0 && r.V == 1 && r.NT == 3 &&
           ((K == 3 && r.R == 3 && r.WY == 16) || (K == 4 && r.R == 2 && r.WY == 16) ||
-           (K == 4 && r.R == 3 && r.WY == 12)))
+           (K == 4 && r.R == 3 && r.WY == 12) || (K == 2 && r.R == 5 && r.WY == 16)))
         r.O = 2;
       break;
     default:

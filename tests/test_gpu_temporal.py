@@ -112,7 +112,7 @@ VARIANTS_K = {3: ["tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5
               4: ["tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6",
                   "tl4:1:6:1:8:0:3", "tl4:1:6:1:8:0:4", "tl4:1:5:1:8:0:3", "tl4:1:6:1:8:7:3",
                   "tl4:1:3:1:12:0:3:2", "tl4:1:3:1:12:0:3"],
-              2: ["tl2", "tl2:1:2:1:16:0:3"]}
+              2: ["tl2", "tl2:1:2:1:16:0:3", "tl2:1:5:1:16:0:3:2"]}
 # fp32 only: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)
 PAIR = {3: ["tl3:2:3:1:16:0:3", "tl3:2:3:1:16:0:3:2", "tl3:2:3:1:16:0:4", "tl3:2:2:1:16:0:3", "tl3:2:3:1:16:5:3"],
         4: ["tl4:2:2:1:16:0:3", "tl4:2:2:1:16:0:4", "tl4:2:2:1:16:7:3"],

@@ -277,13 +277,15 @@ def test_lean_z_stride_model(h3d):
 def test_lean_store_policy_defaults(h3d):
     """Lean sweeps of the default fp64 K = 3 / 4 shapes and of the fp32 K = 3
     pair shape store with the nt cache policy (profiles/nt_stores_r02.md);
-    K = 2 (slower with nt where the solver runs it, profiles/probes_r03.md),
-    other shapes and explicit policies are left as given."""
+    the fp64 K = 2 default is 16 waves x 5 rows with nt stores (80-row tiles,
+    profiles/probes_r04.md); other shapes and explicit policies are left as
+    given."""
     r = h3d.native().kernel_spec_resolved
     assert r("tl3", "fp64") == "tl3:1:3:1:16:0:3:2"
     assert r("tl4", "fp64") == "tl4:1:3:1:12:0:3:2"
     assert r("tl4:1:2:1:16", "fp64") == "tl4:1:2:1:16:0:3:2"
-    assert r("tl2", "fp64") == "tl2:1:3:1:16:0:3"
+    assert r("tl2", "fp64") == "tl2:1:5:1:16:0:3:2"
+    assert r("tl2:1:3:1:16", "fp64") == "tl2:1:3:1:16:0:3"
     assert r("tl3:1:3:1:16:0:3:0", "fp64") == "tl3:1:3:1:16:0:3"
     assert r("tl3:1:3:1:16:0:3:19", "fp64") == "tl3:1:3:1:16:0:3:19"
     assert r("tl3:1:2:1:16", "fp64") == "tl3:1:2:1:16:0:3"
