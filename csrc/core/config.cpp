@@ -115,7 +115,8 @@ std::string Config::usage() {
      << "  --no-block-overlap        block decompositions: exchange the halo first, then sweep\n"
      << "  --no-long-sweeps          step-count remainders as partial sweeps, not K+1-step sweeps\n"
      << "  --long-sweeps auto|on|off remainders as K+1-step sweeps: auto = where the start-up timing of\n"
-     << "                            the sweeps finds them cheaper than a partial sweep (default auto)\n"
+     << "                            the sweeps finds them cheaper than a partial sweep (default auto;\n"
+     << "                            GPU only, measure = on any backend)\n"
      << "  --autotune auto|on|off    time the sweep schedule candidates (z stride, x segments) at start-up;\n"
      << "                            auto: single-subdomain runs (--no-autotune = off)\n"
      << "  --graph-multistream       record the overlapped multi-stream schedule into hipGraphs too\n"
@@ -240,7 +241,8 @@ Config Config::parse(int argc, const char* const* argv) {
       if (v == "auto") c.long_sweeps = -1;
       else if (v == "on") c.long_sweeps = 1;
       else if (v == "off") c.long_sweeps = 0;
-      else throw UsageError("--long-sweeps takes auto, on or off");
+      else if (v == "measure") c.long_sweeps = 2;  // time the sweeps on any backend (tests)
+      else throw UsageError("--long-sweeps takes auto, on, off or measure");
     }
     else if (key == "--no-autotune") c.autotune = 0;
     else if (key == "--autotune") {

@@ -597,8 +597,10 @@ void Solver::calibrate_remainders() {
     long_rem_ = 0;
     return;
   }
-  if (cfg_.long_sweeps > 0 || !be_->is_gpu() || (has_halo_ && !long_halo_) || K_ + 1 > 6) return;
-  {
+  if (cfg_.long_sweeps == 1 || (cfg_.long_sweeps < 0 && !be_->is_gpu()) || (has_halo_ && !long_halo_) ||
+      K_ + 1 > 6)
+    return;
+  if (be_->is_gpu()) {
     KernelSpec kl;
     kl.kind = kspec2_.kind;
     kl.K = K_ + 1;
