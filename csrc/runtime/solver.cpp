@@ -249,7 +249,6 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
         if (dims[a] > 1) hd_[a] = K + 1;
     slot_stride_ = K_ + (long_halo_ ? 1 : 0);
   }
-  halo_depth_ = hd_[0];
   fake_allreduce_us_ = cfg_.fake_allreduce_us;
   chain_ = comm_->ordered_collectives() && !comm_->all_local() && comm_->size() > 1;
   // CU reservation for the overlapped schedule of a real multi-rank job
@@ -590,9 +589,19 @@ void Solver::tune_schedules() {
 // rank times its interior sweeps once at start-up (idempotent sweeps into
 // the next buffer, no residual state, as tune_schedules) and the ranks agree
 // by vote: long for remainder r only where every rank found it cheaper.
+KernelSpec Solver::spec_for_depth(int Kp) const {
+  if (Kp == K_) return kspec2_;
+  if (Kp >= 0 && Kp < 8 && depth_set_[Kp]) return depth_spec_[Kp];
+  KernelSpec ks;
+  ks.kind = kspec2_.kind;
+  ks.K = Kp;
+  return ks;
+}
+
 void Solver::calibrate_remainders() {
   long_rem_ = ~0u;
   sweep_costs_.clear();
+  for (bool& d : depth_set_) d = false;
   if (!tb_ || cfg_.long_sweeps == 0) {
     long_rem_ = 0;
     return;
@@ -608,7 +617,7 @@ void Solver::calibrate_remainders() {
   }
   Event e0 = be_->event_create(), e1 = be_->event_create();
   // Kp = 1: a single step of the owned box; else a sweep of depth Kp
-  auto launch = [&](int Kp) {
+  auto launch = [&](int Kp, const KernelSpec& ks) {
     for (auto& l : local_) {
       StencilParams sp;
       sp.in = l.field[0];
@@ -631,50 +640,81 @@ void Solver::calibrate_remainders() {
       shrink(l.ux, l.sd.n[0], sp.ux);
       shrink(l.uy, l.sd.n[1], sp.uy);
       shrink(l.uz, l.sd.n[2], sp.uz);
-      KernelSpec ks = kspec2_;
-      if (Kp != K_) {
-        ks = KernelSpec();
-        ks.kind = kspec2_.kind;
-        ks.K = Kp;
-      }
       be_->sweep(dt_, sp, ks, kCompute);
     }
   };
+  // candidates: the K and K+1 sweeps, a single step, the partial sweeps;
+  // fp64 K = 2 in two tile shapes: 80-row tiles (fewer halo rows per stored
+  // one, the kernel-level winner) and 48-row ones (a 122-plane slab share on
+  // 248 CUs takes 252 of the tall tiles = two rounds, 450 short ones also
+  // two: the short ones won there, 0.52 against 0.70 ms)
+  struct Cand {
+    int Kp;
+    KernelSpec ks;
+    std::string name;
+  };
+  std::vector<Cand> cands{{K_, kspec2_, "sweep" + std::to_string(K_)},
+                          {K_ + 1, spec_for_depth(K_ + 1), "sweep" + std::to_string(K_ + 1)}};
+  for (int r = 1; r < K_; ++r) {
+    if (r == 2 && dt_ == DType::F64 && kspec2_.kind == KernelSpec::TBL && be_->is_gpu()) {
+      for (const char* v : {"tl2:1:5:1:16:0:3:2", "tl2:1:3:1:16:0:3:2"}) {
+        const KernelSpec ks = KernelSpec::parse(v);
+        if (hip::lean_supported(dt_, ks)) cands.push_back({2, ks, std::string("sweep2[") + v + "]"});
+      }
+      continue;
+    }
+    cands.push_back({r, r == 1 ? kspec_ : spec_for_depth(r), r == 1 ? std::string("step") : "sweep" + std::to_string(r)});
+  }
   // the GPU is cold here (initialisation, no sweeps yet): keep it busy with
   // regular sweeps for >= 30 ms before timing, then take the best of two
   // interleaved rounds per candidate (a cold first timing inflated the
   // 8-GPU share's K = 3 sweep by 20% and flipped the decision)
-  std::vector<int> cands{K_, K_ + 1};
-  for (int r = 1; r < K_; ++r) cands.push_back(r);
   std::vector<double> best(cands.size(), 1e30);
   {
     be_->record(e0, kCompute);
-    launch(K_);
+    launch(K_, kspec2_);
     be_->record(e1, kCompute);
     be_->sync(kCompute);
     const double one = std::max(1e-3, (double)be_->elapsed_ms(e0, e1));
     const int warm = std::max(1, std::min(200, (int)std::ceil(30.0 / one)));
-    for (int i = 0; i < warm; ++i) launch(K_);
+    for (int i = 0; i < warm; ++i) launch(K_, kspec2_);
   }
   constexpr int reps = 3;
   for (int round = 0; round < 2; ++round)
     for (std::size_t c = 0; c < cands.size(); ++c) {
       be_->record(e0, kCompute);
-      for (int i = 0; i < reps; ++i) launch(cands[c]);
+      for (int i = 0; i < reps; ++i) launch(cands[c].Kp, cands[c].ks);
       be_->record(e1, kCompute);
       be_->sync(kCompute);
       best[c] = std::min(best[c], (double)be_->elapsed_ms(e0, e1) / reps);
     }
-  for (std::size_t c = 0; c < cands.size(); ++c)
-    sweep_costs_.push_back({cands[c] == 1 ? std::string("step") : "sweep" + std::to_string(cands[c]), best[c]});
-  const double tk = best[0], tl = best[1];
   be_->event_destroy(e0);
   be_->event_destroy(e1);
+  // per depth: the fastest candidate (a rank-local kernel choice: the halo
+  // of a partial sweep does not depend on its tile shape)
+  std::vector<double> cost(K_ + 2, 1e30);
+  for (std::size_t c = 0; c < cands.size(); ++c) {
+    sweep_costs_.push_back({cands[c].name, best[c]});
+    const int Kp = cands[c].Kp;
+    if (best[c] < cost[Kp]) {
+      cost[Kp] = best[c];
+      if (Kp != K_ && Kp > 1) {
+        depth_spec_[Kp] = cands[c].ks;
+        depth_set_[Kp] = true;
+      }
+    }
+  }
+  for (int Kp = 2; Kp < K_; ++Kp)
+    if (cands.size() && cost[Kp] < 1e30 && std::count_if(cands.begin(), cands.end(), [&](const Cand& c) {
+          return c.Kp == Kp;
+        }) > 1)
+      sweep_costs_.push_back({"sweep" + std::to_string(Kp), cost[Kp]});
+  const double tk = cost[K_], tl = cost[K_ + 1];
   // votes for the partial sweep, one slot per remainder; the ranks agree on
   // the max: long only where no rank found the partial sweep cheaper (the
   // halo depth of every exchange must match between neighbours)
   std::vector<unsigned long long> partial(K_, 0);
-  for (int r = 1; r < K_; ++r) partial[r] = r * (tl - tk) < best[1 + r] ? 0 : 1;
+  for (int r = 1; r < K_; ++r) partial[r] = r * (tl - tk) < cost[r] ? 0 : 1;
   if (!comm_->all_local() && comm_->size() > 1) {
     void* d = be_->alloc(sizeof(unsigned long long) * K_);
     be_->copy(d, partial.data(), sizeof(unsigned long long) * K_, CopyKind::H2D, kReduce);
@@ -909,14 +949,9 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   // lagged schedule: events and residual slots alternate by sweep parity
   const int q = lag_ ? (int)(nsweep_ & 1) : bi;
   const int slot0 = lag_ ? q * slot_stride_ : 0;
-  KernelSpec ks = kspec2_;
-  if (Kp != K_) {
-    // partial (Kp < K) or long (Kp = K + 1, single subdomain) sweep: the
-    // kernel family's default variant of depth Kp
-    ks = KernelSpec();
-    ks.kind = kspec2_.kind;
-    ks.K = Kp;
-  }
+  // partial (Kp < K) or long (Kp = K + 1) sweeps: the kernel family's default
+  // variant of depth Kp, or the one the start-up timing kept
+  const KernelSpec ks = spec_for_depth(Kp);
   // update ranges reach Kp - 1 (not K_ - 1) points into the deep halos
   auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
     o[0] = u[0] < 0 ? -(Kp - 1) : u[0];
@@ -1421,8 +1456,6 @@ void Solver::synchronize() {
   be_->sync_all();
   comm_->check_async_error();
 }
-
-void Solver::poll_enqueue(StreamId s) { (void)s; }
 
 HostState Solver::state() {
   be_->sync_all();

@@ -251,7 +251,6 @@ class Solver {
   int prv(int b) const { return b == 0 ? nbuf_ - 1 : b - 1; }
   void record_segment(int64_t start, int len, int inbuf);
   void finalize_converged(int64_t conv_iter);
-  void poll_enqueue(StreamId s);
   void ev_record(int id, StreamId s);
   void ev_wait(StreamId s, int id);
   void run_chunk(int64_t n);
@@ -275,7 +274,6 @@ class Solver {
   bool has_halo_ = false;  // any face with a neighbour on any local subdomain
   bool overlap_ = true;
   bool tb_overlap_ = false;   // sweeps: interior || (deep halo -> boundary slabs)
-  int halo_depth_ = 1;        // x-face ghost planes (K, or K+1 with long_halo_)
   int64_t hd_[3] = {1, 1, 1}; // ghost depth per axis (K on split axes with temporal blocking, K+1 with long_halo_)
   int64_t xd_[3] = {1, 1, 1}; // regular exchange depth per axis (K on split axes with temporal blocking)
   // Long sweeps (depth K+1) across halos: ghosts allocated K+1 deep on split
@@ -286,6 +284,11 @@ class Solver {
   // remainder policy (long_sweeps_for): bit r set = a step count with n mod K
   // = r ends in r long sweeps, else in a partial sweep of r steps
   unsigned long_rem_ = ~0u;
+  // kernel of a sweep of depth Kp != K (partial / long): the family default,
+  // or the variant the start-up timing kept (depth_spec_[Kp] where depth_set_)
+  KernelSpec depth_spec_[8];
+  bool depth_set_[8] = {};
+  KernelSpec spec_for_depth(int Kp) const;
   std::vector<std::pair<std::string, double>> sweep_costs_;  // start-up timings (ms per sweep)
   void calibrate_remainders();
   int last_bnd_ = 0;          // boundary-layer depth of the last overlapped sweep (0: none pending)

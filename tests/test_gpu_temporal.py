@@ -545,7 +545,10 @@ def test_remainder_policy_measured_gpu(h3d, gpu, vr, dims):
     b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="hip", extra_args=["--temporal", "1"])
     a.initialize(), b.initialize()
     costs = a.native.sweep_costs
-    assert set(costs) == {"sweep3", "sweep4", "step", "sweep2"} and all(v > 0 for v in costs.values()), costs
+    assert {"sweep3", "sweep4", "step", "sweep2"} <= set(costs) and all(v > 0 for v in costs.values()), costs
+    # fp64 K = 2: both tile shapes timed, the partial sweep costs the faster one
+    shapes = [k for k in costs if k.startswith("sweep2[")]
+    assert len(shapes) == 2 and costs["sweep2"] == min(costs[k] for k in shapes), costs
     rem = a.native.long_remainders
     for r in (1, 2):
         assert (r in rem) == (r * (costs["sweep4"] - costs["sweep3"]) < costs["step" if r == 1 else "sweep2"]), \

@@ -40,6 +40,12 @@ def main() -> int:
     ap.add_argument("--preheat-ms", type=float, default=0.0,
                     help="as bench.py --preheat-ms: untimed idempotent sweeps right before the timed window "
                          "(the driver-config rehearsal: --steps 20 --warmup 5 --preheat-ms 20)")
+    ap.add_argument("--idle-ms", type=float, default=0.0,
+                    help="diagnostic: host sleep between the synchronised warm-up / preheat and the timed window "
+                         "(the GPU idles that long; does the first timed sweep slow down?)")
+    ap.add_argument("--no-sync", action="store_true",
+                    help="diagnostic: do not synchronise between the preheat and the timed window (the timed window "
+                         "then also waits for the preheat's tail: not a valid timing, a trace-shape probe)")
     ap.add_argument("--trace-schedule", action="store_true",
                     help="print the start-up schedule tuner's candidate timings (HEAT3D_TRACE, read once: on for the whole run)")
     args = ap.parse_args()
@@ -73,7 +79,10 @@ def main() -> int:
         K = s.native.temporal_steps
         est_ms = s.interior_points / P * max(1, K) / (800e9 if args.dtype == "fp64" else 1400e9) * 1e3
         preheat = s.native.preheat(max(1, min(64, int(args.preheat_ms / max(est_ms, 1e-3)) + 1)))
-        s.synchronize()
+        if not args.no_sync:
+            s.synchronize()
+    if args.idle_ms > 0:
+        time.sleep(args.idle_ms / 1e3)
     t0 = time.perf_counter()
     s.step(args.steps)
     s.synchronize()
