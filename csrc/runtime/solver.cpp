@@ -230,6 +230,9 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   // K+1 deep on split axes; only a long sweep exchanges K+1 planes.  Needs
   // K+1 owned points per split axis (2(K+1)+1 when overlapped), the K+1
   // kernel, and two banks of K+1 residual slots under the lagged check.
+  // Whether a remainder actually runs as long sweeps is decided per run by
+  // timing the sweeps at start-up (calibrate_remainders): on the 8-GPU slab
+  // share a K+1 sweep costs 1.65-1.73x a K one.
   {
     bool ok = tb_ && has_split && cfg_.long_sweeps && K + 1 <= 6 && K + 1 <= kResidualSlots &&
               (!lag_ || 2 * (K + 1) <= kResidualSlots);
@@ -1011,16 +1014,62 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   // previous sweep's boundary slabs (comm-stream order) — unless they were
   // thinner than d, when the previous interior wrote the rest: wait for it
   // (a long sweep right after a K-thick one, e.g. across step() calls)
+  const int prev_bnd = last_bnd_;
   if (last_bnd_ > 0 && (dv ? K_ + 1 : K_) > last_bnd_) ev_wait(kComm, EV_INT + (q ^ 1));
   last_bnd_ = lb ? K_ + 1 : K_;
   enqueue_halo(bi, kComm, dv);
   flush_pending_reduce();
-  // [A] interior planes
+  // [A] interior planes, as a core and a rim.  The core's Kp-step cone
+  // reads only planes the previous sweep's interior wrote (>= prev_bnd from
+  // every face with a neighbour), so it starts as soon as that interior is
+  // done; the rim (Kp planes inside the interior's faces) also reads the
+  // previous boundary slabs and waits for them.  Without the split the whole
+  // interior waited for the previous sweep's halo + boundary chain (8-GPU
+  // slab share: ~90 us idle per sweep, profiles/rank_proxy_r04.md).  Writes
+  // stay disjoint from what the previous boundary slabs still read: they
+  // reach at most prev_bnd + Kp - 1 planes in.
   ev_wait(kCompute, EV_CHK + chk_prev);
-  ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of our input
   be_->range_push("interior");
   prof_record(prof_idx_, PE_INT0, kCompute);
-  for (auto& l : local_) be_->sweep(dt_, params(l, lb ? l.tb_interior_long : l.tb_interior), ks, kCompute);
+  bool split = prev_bnd > 0 && cfg_.core_rim;
+  std::vector<std::pair<Box, std::vector<Box>>> parts;  // per local: core, rim pieces
+  for (auto& l : local_) {
+    const Box& ib = lb ? l.tb_interior_long : l.tb_interior;
+    Box core = ib;
+    for (int a = 0; a < 3; ++a) {
+      if (hd_[a] <= 1) continue;
+      if (l.sd.has_neighbor(static_cast<Face>(2 * a))) core.lo[a] = std::max(core.lo[a], (int64_t)(prev_bnd + Kp));
+      if (l.sd.has_neighbor(static_cast<Face>(2 * a + 1)))
+        core.hi[a] = std::min(core.hi[a], l.sd.n[a] - (prev_bnd + Kp));
+    }
+    std::vector<Box> rim;
+    Box rem = ib;
+    for (int a = 0; a < 3 && !core.empty(); ++a) {
+      if (core.lo[a] > rem.lo[a]) {
+        Box p = rem;
+        p.hi[a] = core.lo[a];
+        rim.push_back(p);
+        rem.lo[a] = core.lo[a];
+      }
+      if (core.hi[a] < rem.hi[a]) {
+        Box p = rem;
+        p.lo[a] = core.hi[a];
+        rim.push_back(p);
+        rem.hi[a] = core.hi[a];
+      }
+    }
+    split &= !core.empty();
+    parts.push_back({core, rim});
+  }
+  if (split) {
+    for (std::size_t i = 0; i < local_.size(); ++i) be_->sweep(dt_, params(local_[i], parts[i].first), ks, kCompute);
+    ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of the rim's input
+    for (std::size_t i = 0; i < local_.size(); ++i)
+      for (const Box& b : parts[i].second) be_->sweep(dt_, params(local_[i], b), ks, kCompute);
+  } else {
+    ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of our input
+    for (auto& l : local_) be_->sweep(dt_, params(l, lb ? l.tb_interior_long : l.tb_interior), ks, kCompute);
+  }
   prof_record(prof_idx_, PE_INT1, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
