@@ -114,7 +114,8 @@ std::string Config::usage() {
      << "  --lag auto|on|off         lagged convergence check of overlapped sweeps (3rd field buffer)\n"
      << "  --no-block-overlap        block decompositions: exchange the halo first, then sweep\n"
      << "  --no-long-sweeps          step-count remainders as partial sweeps, not K+1-step sweeps\n"
-     << "  --no-core-rim             overlapped sweeps: the whole interior waits for the previous boundary slabs\n"
+     << "  --core-rim                overlapped sweeps: interior as a core that does not wait for the previous\n"
+     << "                            boundary slabs plus a rim that does (opt-in; --no-core-rim: off, default)\n"
      << "  --long-sweeps auto|on|off remainders as K+1-step sweeps: auto = where the start-up timing of\n"
      << "                            the sweeps finds them cheaper than a partial sweep (default auto;\n"
      << "                            GPU only, measure = on any backend)\n"
@@ -238,6 +239,7 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--no-block-overlap") c.block_overlap = false;
     else if (key == "--no-long-sweeps") c.long_sweeps = 0;
     else if (key == "--no-core-rim") c.core_rim = false;
+    else if (key == "--core-rim") c.core_rim = true;
     else if (key == "--long-sweeps") {
       const std::string v = get("--long-sweeps");
       if (v == "auto") c.long_sweeps = -1;

@@ -68,8 +68,9 @@ struct Config {
   int verbose = 0;
   double progress_s = 0;          // run(): stderr heartbeat period (0 = off)
   double time_limit_s = 0;        // run(): wall budget, stop unconverged past it (0 = none)
-  bool core_rim = true;           // overlapped sweeps: interior as a core (not waiting for the previous
-                                  // boundary slabs) and a rim (waiting for them)
+  bool core_rim = false;          // overlapped sweeps: interior as a core (not waiting for the previous
+                                  // boundary slabs) and a rim (waiting for them); measured slower
+                                  // in the 8-GPU proxy (profiles/rank_proxy_r04.md), opt-in
   bool quiet = false;
   int cpu_threads = 0;
   int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules

@@ -497,14 +497,16 @@ def test_preheat_keeps_rollback_input_gpu(h3d, gpu, vr, dims):
 
 
 @pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (8, 1, 1)), (8, (2, 2, 2)), (4, (1, 2, 2))])
-@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
-def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype):
+@pytest.mark.parametrize("dtype,core_rim", [("fp64", False), ("fp32", False), ("fp64", True)])
+def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype, core_rim):
     """The driver's window at N > 1 (warm-up 5, then 20 steps = 4 x 3 + 2 x 4):
     long K+1 sweeps across the halos, including the (K+1)-plane boundary
-    slabs (y-marching K = 4 thin-slab tiles), bitwise equal to single steps."""
+    slabs (y-marching K = 4 thin-slab tiles), bitwise equal to single steps;
+    also with ``--core-rim`` (interior as core + rim, rims wait for the
+    previous boundary slabs on the device)."""
     n = (82, 70, 150)
     a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims,
-                       extra_args=["--long-sweeps", "on"])
+                       extra_args=["--long-sweeps", "on"] + (["--core-rim"] if core_rim else []))
     b = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
     assert a.native.long_halo_sweeps
     a.initialize(), b.initialize()

@@ -385,16 +385,17 @@ LONG_HALO = [(3, (3, 1, 1)), (2, (2, 1, 1)), (4, (2, 2, 1)), (8, (2, 2, 2)), (3,
 
 
 @pytest.mark.parametrize("vr,dims", LONG_HALO)
-@pytest.mark.parametrize("K", [2, 3])
-def test_long_sweeps_across_halos(h3d, vr, dims, K):
+@pytest.mark.parametrize("K,core_rim", [(2, False), (3, False), (3, True)])
+def test_long_sweeps_across_halos(h3d, vr, dims, K, core_rim):
     """Step counts that are not multiples of K end in sweeps of depth K+1
     across the halos (ghosts K+1 deep on split axes, exchanged K+1 deep
     before a long sweep only) — the driver's 20-step window at N > 1 runs
     4 x 3 + 2 x 4 instead of 6 x 3 + a partial 2 — bitwise equal to single
-    steps for every count, mixed with regular sweeps on the same fields."""
+    steps for every count, mixed with regular sweeps on the same fields.
+    ``--core-rim``: the interiors split into core + rim pieces."""
     n = (33, 29, 31)
     a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", virtual_ranks=vr, decomp=dims,
-                       extra_args=["--temporal", str(K)])
+                       extra_args=["--temporal", str(K)] + (["--core-rim"] if core_rim else []))
     b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", extra_args=T1)
     assert a.native.long_halo_sweeps
     assert list(a.native.ghost_depth) == [K + 1 if d > 1 else 1 for d in dims]
