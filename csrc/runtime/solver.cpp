@@ -2019,9 +2019,15 @@ void Solver::save_checkpoint(const std::string& dir) {
       const int64_t ey = g.extent(1), ez = g.extent(2);
       stream_box_out(*be_, dt_, esize_, l.field[p], l.L, l.sd, g, io_stage_bytes(cfg_), [&](int64_t x0, int64_t nx, const char* h) {
         sum += host_bitsum(h, nx * ey * ez, dt_);
+        // contiguous runs in the file: the whole chunk (x slabs), a plane's
+        // rows (y splits), else one row at a time (z splits)
+        if (ez == N[2] && ey == N[1]) {
+          io::pwrite_all(fd, h, nx * ey * ez * esize_, (g.lo[0] + x0) * N[1] * N[2] * esize_);
+          return;
+        }
         for (int64_t i = 0; i < nx; ++i) {
           const int64_t gi = g.lo[0] + x0 + i;
-          if (ez == N[2] && ey == N[1]) {  // whole planes: one contiguous run
+          if (ez == N[2]) {
             io::pwrite_all(fd, h + i * ey * ez * esize_, ey * ez * esize_, (gi * N[1] + g.lo[1]) * N[2] * esize_);
             continue;
           }

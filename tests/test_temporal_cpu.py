@@ -240,7 +240,8 @@ def test_block_overlap_matches_exchange_first(h3d, dims):
         assert np.array_equal(a.gather(), b.gather())
 
 
-@pytest.mark.parametrize("dims_a,dims_b", [((2, 2, 2), (1, 1, 1)), ((1, 1, 1), (2, 2, 1)), ((3, 1, 1), (1, 2, 2))])
+@pytest.mark.parametrize("dims_a,dims_b", [((2, 2, 2), (1, 1, 1)), ((1, 1, 1), (2, 2, 1)), ((3, 1, 1), (1, 2, 2)),
+                                           ((1, 3, 1), (2, 1, 1))])
 def test_checkpoint_restart_across_temporal_decompositions(h3d, tmp_path, dims_a, dims_b):
     """A checkpoint written by a temporally blocked run (three buffers when
     overlapped) restarts on any other decomposition and finishes at the same
