@@ -68,6 +68,10 @@ struct Config {
   int verbose = 0;
   double progress_s = 0;          // run(): stderr heartbeat period (0 = off)
   double time_limit_s = 0;        // run(): wall budget, stop unconverged past it (0 = none)
+  // overlapped x-slab sweeps: the halo travels in M row chunks and the
+  // boundary slabs of each chunk start as soon as it (and the next) landed,
+  // on their own stream (0 = auto, 1 = one piece)
+  int halo_chunks = 0;
   bool core_rim = false;          // overlapped sweeps: interior as a core (not waiting for the previous
                                   // boundary slabs) and a rim (waiting for them); measured slower
                                   // in the 8-GPU proxy (profiles/rank_proxy_r04.md), opt-in

@@ -715,6 +715,7 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("field_buffers", &Solver::field_buffers)
       .def_property_readonly("ghost_depth", &Solver::ghost_depth)
       .def_property_readonly("long_halo_sweeps", &Solver::long_halo_sweeps)
+      .def_property_readonly("halo_chunks", &Solver::halo_chunks)
       .def_property_readonly("long_remainders",
                              [](const Solver& s) {
                                std::vector<int> r;

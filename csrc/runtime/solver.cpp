@@ -325,6 +325,27 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     local_.push_back(l);
   }
   setup_faces();
+  // chunked halo pipeline: overlapped sweeps whose every face is an x face
+  // sent in place or copied locally (x-slab decompositions), bands of at
+  // least K+2 rows so that a band's boundary cone reaches one band further
+  {
+    // (the lagged check: the slabs are issued before the previous sweep's
+    // check, which they need not wait for only when it is two sweeps back)
+    bool ok = tb_overlap_ && lag_ && !ordered_halo_ && cfg_.halo_chunks != 1;
+    int64_t ny = INT64_MAX;
+    for (const auto& l : local_) {
+      ny = std::min(ny, l.sd.n[1]);
+      for (const auto& io : l.faces) ok &= face_axis(io.face) == 0 && (io.contiguous || io.peer_local >= 0);
+    }
+    int M = cfg_.halo_chunks > 1 ? cfg_.halo_chunks : 1;
+    while (M > 1 && ny / M < K_ + 3) --M;
+    if (ok && M > 1) {
+      // every local subdomain of an x-slab decomposition has the same ny
+      for (const auto& l : local_) ok &= l.sd.n[1] == ny;
+      hch_ = ok ? M : 1;
+      for (int c = 0; c <= hch_ && hch_ > 1; ++c) ych_.push_back(ny * c / hch_);
+    }
+  }
   dstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
   hstate_ = static_cast<DeviceState*>(be_->alloc_host(2 * sizeof(DeviceState)));
   std::memset(hstate_, 0, 2 * sizeof(DeviceState));
@@ -793,7 +814,15 @@ void Solver::enqueue_halo(int p, StreamId s, int dv) {
 }
 
 template <typename Pred>
-void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase) {
+void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase, int64_t ylo, int64_t yhi) {
+  const bool band = ylo != INT64_MIN || yhi != INT64_MAX;
+  auto rows = [&](Box b) {  // a face box restricted to the band (x faces span the owned rows)
+    if (band) {
+      b.lo[1] = std::max(b.lo[1], ylo);
+      b.hi[1] = std::min(b.hi[1], yhi);
+    }
+    return b;
+  };
   if (comm_->all_local()) {
     for (auto& l : local_)
       for (auto& io : l.faces) {
@@ -803,7 +832,7 @@ void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase) {
         for (auto& nio : nb.faces)
           if (nio.face == opposite(io.face)) src = &nio.g[dv].send_box;
         HEAT3D_CHECK(src, "opposite face missing");
-        be_->copy_box(dt_, nb.field[p], nb.L, *src, l.field[p], l.L, io.g[dv].recv_box, s);
+        be_->copy_box(dt_, nb.field[p], nb.L, rows(*src), l.field[p], l.L, rows(io.g[dv].recv_box), s);
       }
   } else {
     std::vector<Transfer> xs;
@@ -812,6 +841,28 @@ void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase) {
       for (auto& io : l.faces) {
         if (!in_phase(io)) continue;
         const FaceGeom& fg = io.g[dv];
+        if (band) {
+          // x planes in place, one transfer per plane: layout rows [r0, r1)
+          // (the ghost rows ride with the first / last band)
+          HEAT3D_CHECK(io.contiguous && face_axis(io.face) == 0, "halo bands need in-place x faces");
+          const int64_t r0 = ylo <= 0 ? -l.L.gy : ylo, r1 = yhi >= l.sd.n[1] ? l.sd.n[1] + l.L.gy : yhi;
+          const int64_t bytes = (r1 - r0) * l.L.sy * (int64_t)esize_;
+          const int64_t np = fg.send_box.hi[0] - fg.send_box.lo[0];
+          for (int64_t i = 0; i < np; ++i) {
+            Transfer snd, rcv;
+            snd.src_rank = l.sd.rank;
+            snd.dst_rank = io.peer;
+            snd.src = base + (l.L.plane_offset(fg.send_box.lo[0] + i) + (r0 + l.L.gy) * l.L.sy) * esize_;
+            snd.bytes = bytes;
+            rcv.src_rank = io.peer;
+            rcv.dst_rank = l.sd.rank;
+            rcv.dst = base + (l.L.plane_offset(fg.recv_box.lo[0] + i) + (r0 + l.L.gy) * l.L.sy) * esize_;
+            rcv.bytes = bytes;
+            xs.push_back(snd);
+            xs.push_back(rcv);
+          }
+          continue;
+        }
         if (!io.contiguous) be_->pack_box(dt_, l.field[p], l.L, fg.send_box, io.sendbuf, s);
         Transfer snd, rcv;
         snd.src_rank = l.sd.rank;
@@ -1017,7 +1068,44 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   const int prev_bnd = last_bnd_;
   if (last_bnd_ > 0 && (dv ? K_ + 1 : K_) > last_bnd_) ev_wait(kComm, EV_INT + (q ^ 1));
   last_bnd_ = lb ? K_ + 1 : K_;
-  enqueue_halo(bi, kComm, dv);
+  const StreamId sb = bnd_stream();
+  auto boundary_boxes = [&](Local& l) -> const std::vector<Box>& { return lb ? l.tb_boundary_long : l.tb_boundary; };
+  if (hch_ <= 1) {
+    enqueue_halo(bi, kComm, dv);
+  } else {
+    // [B1+B2] chunked: band c of the halo, then (boundary stream) the boundary
+    // slabs of band c-1, whose Kp-step cone reaches Kp rows into band c.
+    // Band c of the halo sends rows the previous sweep's boundary slabs of
+    // band c wrote (EV_BCH + c).  The slabs overwrite planes of nxt(bi): the
+    // previous interior read them (2 buffers) and the previous halo sent them
+    // (done: it precedes band c+1 on the comm stream).
+    ev_wait(sb, EV_INT + (q ^ 1));
+    ev_wait(sb, EV_CHK + chk_prev);
+    auto slabs = [&](int c) {
+      ev_wait(sb, EV_HCH + std::min(c + 1, hch_ - 1));
+      if (c == 0) prof_record(prof_idx_, PE_BND0, sb);
+      for (auto& l : local_)
+        for (Box b : boundary_boxes(l)) {
+          b.lo[1] = std::max(b.lo[1], ych_[c]);
+          b.hi[1] = std::min(b.hi[1], ych_[c + 1]);
+          if (!b.empty()) be_->sweep(dt_, params(l, b), ks, sb);
+        }
+      ev_record(EV_BCH + c, sb);
+    };
+    be_->range_push("halo");
+    prof_record(prof_idx_, PE_HALO0, kComm);
+    for (int c = 0; c < hch_; ++c) {
+      ev_wait(kComm, EV_BCH + c);
+      enqueue_halo_phase(bi, kComm, dv, [](const FaceIO&) { return true; }, ych_[c], ych_[c + 1]);
+      ev_record(EV_HCH + c, kComm);
+      if (c > 0) slabs(c - 1);
+    }
+    prof_record(prof_idx_, PE_HALO1, kComm);
+    be_->range_pop();
+    slabs(hch_ - 1);
+    prof_record(prof_idx_, PE_BND1, sb);
+    ev_record(EV_BND + q, sb);
+  }
   flush_pending_reduce();
   // [A] interior planes, as a core and a rim.  The core's Kp-step cone
   // reads only planes the previous sweep's interior wrote (>= prev_bnd from
@@ -1073,17 +1161,18 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   prof_record(prof_idx_, PE_INT1, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
-  // [B2] the boundary slabs, behind the halo on the comm stream
-  ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
-  ev_wait(kComm, EV_CHK + chk_prev);
-  be_->range_push("boundary");
-  prof_record(prof_idx_, PE_BND0, kComm);
-  for (auto& l : local_) {
-    for (const Box& b : lb ? l.tb_boundary_long : l.tb_boundary) be_->sweep(dt_, params(l, b), ks, kComm);
+  if (hch_ <= 1) {
+    // [B2] the boundary slabs, behind the halo on the comm stream
+    ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
+    ev_wait(kComm, EV_CHK + chk_prev);
+    be_->range_push("boundary");
+    prof_record(prof_idx_, PE_BND0, kComm);
+    for (auto& l : local_)
+      for (const Box& b : boundary_boxes(l)) be_->sweep(dt_, params(l, b), ks, kComm);
+    prof_record(prof_idx_, PE_BND1, kComm);
+    be_->range_pop();
+    ev_record(EV_BND + q, kComm);
   }
-  prof_record(prof_idx_, PE_BND1, kComm);
-  be_->range_pop();
-  ev_record(EV_BND + q, kComm);
   // [C] all residuals, all checks: now, or (ordered collectives) after the
   // next sweep's halo.  With the lag nothing waits for CHK(q) before sweep
   // q+2; without it sweep q+1's interior does, and is issued after the flush.
@@ -1112,12 +1201,13 @@ void Solver::flush_pending_reduce() {
   if (!pending_.valid) return;
   pending_.valid = false;
   const int q = pending_.q;
-  ev_wait(kReduce, EV_INT + q);
-  ev_wait(kReduce, EV_BND + q);
-  prof_record(pending_.prof, PE_RED0, kReduce);
-  reduce_and_check(kReduce, pending_.slot0, pending_.Kp, pending_.prof);
-  prof_record(pending_.prof, PE_CHK1, kReduce);
-  ev_record(EV_CHK + q, kReduce);
+  const StreamId sr = red_stream();
+  ev_wait(sr, EV_INT + q);
+  ev_wait(sr, EV_BND + q);
+  prof_record(pending_.prof, PE_RED0, sr);
+  reduce_and_check(sr, pending_.slot0, pending_.Kp, pending_.prof);
+  prof_record(pending_.prof, PE_CHK1, sr);
+  ev_record(EV_CHK + q, sr);
 }
 
 void Solver::prof_record(int sweep, int id, StreamId s) {

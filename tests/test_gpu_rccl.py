@@ -42,6 +42,8 @@ def test_rccl_self_exchange(ext, gpu):
     (2, (2, 1, 1), None),
     (2, (2, 1, 1), ["--rccl-shared"]),               # one communicator for halos and all-reduce
     (4, (2, 2, 1), None),                             # block: deep y halos, axis-ordered phases
+    (2, (2, 1, 1), ["--halo-chunks", "4"]),           # halo in row bands, boundary slabs per band
+    (3, (3, 1, 1), ["--halo-chunks", "3"]),
 ])
 def test_rccl_multirank_bitwise(h3d, gpu, tmp_path, world, decomp, extra):
     n, eps = 33, 1e-4
@@ -52,7 +54,7 @@ def test_rccl_multirank_bitwise(h3d, gpu, tmp_path, world, decomp, extra):
     r1 = single.run()
     it, err, name, graphs = open(tmp_path / "result.txt").read().split()
     assert int(it) == r1["conv_iter"]  # the same stopping iteration as one rank
-    assert name == ("rccl(shared)" if extra else "rccl")
+    assert name == ("rccl(shared)" if extra and "--rccl-shared" in extra else "rccl")
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
 
 

@@ -410,6 +410,41 @@ def test_long_sweeps_across_halos(h3d, vr, dims, K, core_rim):
     assert a.native.verify_halos() == 0
 
 
+@pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (2, (2, 1, 1)), (4, (4, 1, 1))])
+@pytest.mark.parametrize("K,M", [(2, 4), (3, 2), (3, 3)])
+def test_chunked_halo_pipeline(h3d, vr, dims, K, M):
+    """--halo-chunks M: the x-slab halo as M row bands, each band's boundary
+    slabs as soon as it and the next one landed, with regular, partial and
+    long sweeps; bitwise equal to single steps."""
+    n = (40, 37, 31)
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", virtual_ranks=vr, decomp=dims,
+                       extra_args=["--temporal", str(K), "--halo-chunks", str(M)])
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", extra_args=T1)
+    assert a.native.halo_chunks == M
+    a.initialize(), b.initialize()
+    for k in (5, 20, 7, 11, 4):
+        a.step(k)
+        b.step(k)
+        sa, sb = a.native.state(), b.native.state()
+        assert sa["iter"] == sb["iter"] and sa["last_residual"] == sb["last_residual"]
+        assert np.array_equal(a.gather(), b.gather()), (vr, dims, K, M, k)
+    assert a.native.verify_halos() == 0
+
+
+def test_chunked_halo_fallbacks(h3d):
+    """Bands need x faces only, the lagged check and >= K + 3 rows each: block
+    decompositions, thin slabs and --halo-chunks 1 run the single exchange."""
+    def chunks(dims, n, M, extra=()):
+        s = h3d.HeatSolver(n, 10, 0.0, backend="cpu", virtual_ranks=dims[0] * dims[1] * dims[2], decomp=dims,
+                           extra_args=["--temporal", "3", "--halo-chunks", str(M), *extra])
+        return s.native.halo_chunks
+    assert chunks((2, 1, 1), (40, 37, 31), 4) == 4
+    assert chunks((2, 1, 1), (40, 37, 31), 1) == 1
+    assert chunks((2, 2, 1), (40, 37, 31), 4) == 1
+    assert chunks((2, 1, 1), (40, 14, 31), 4) == 2   # 12 owned rows: bands of >= 6
+    assert chunks((2, 1, 1), (40, 37, 31), 4, ["--lag", "off"]) == 1
+
+
 def test_long_sweeps_across_halos_off(h3d):
     """--no-long-sweeps keeps K-deep ghosts (remainders as partial sweeps)."""
     a = h3d.HeatSolver((33, 29, 31), 20, 0.0, backend="cpu", virtual_ranks=3, decomp=(3, 1, 1),
