@@ -91,6 +91,11 @@ std::unique_ptr<Comm> make_staged_comm(std::unique_ptr<Comm> inner);
 struct PhantomOptions {
   double gbps = 50.0, allreduce_us = 20.0;
   int channels = 4, allreduce_channels = 2;
+  // false: an exchange is its wire time (bytes / gbps) followed by the D2D
+  // copies that stand in for the data; true: the copies run inside the wire
+  // time (an exchange lasts max(wire, copies)), as a transport that moves the
+  // data while it is on the wire
+  bool overlap_copies = false;
 };
 std::unique_ptr<Comm> make_phantom_comm(int rank, int size, const PhantomOptions& o = {});
 

@@ -26,8 +26,11 @@ class PhantomComm final : public Comm {
  public:
   PhantomComm(int rank, int size, const PhantomOptions& o)
       : rank_(rank), size_(size), gbps_(o.gbps), ar_us_(o.allreduce_us), channels_(o.channels),
-        ar_channels_(o.allreduce_channels) {
+        ar_channels_(o.allreduce_channels), overlap_(o.overlap_copies) {
     HEAT3D_CHECK(rank >= 0 && rank < size, "phantom rank " << rank << " of " << size);
+  }
+  ~PhantomComm() override {
+    if (slot_ && be_) be_->release(slot_);
   }
   const char* name() const override { return "phantom"; }
   int size() const override { return size_; }
@@ -43,7 +46,17 @@ class PhantomComm final : public Comm {
     std::size_t worst = 0;
     for (const auto& kv : per_peer) worst = std::max(worst, kv.second);
     // bytes / (GB/s) in us, every peer's channels in flight at once
-    if (worst && gbps_ > 0) be.delay(worst / (gbps_ * 1e3), s, channels_ * (int)per_peer.size());
+    const double wire = worst && gbps_ > 0 ? worst / (gbps_ * 1e3) : 0.0;
+    const int blocks = channels_ * (int)per_peer.size();
+    if (overlap_ && wire > 0) {
+      if (!slot_) {
+        be_ = &be;
+        slot_ = be.alloc(8);
+      }
+      be.stamp(slot_, s);
+    } else if (wire > 0) {
+      be.delay(wire, s, blocks);
+    }
     for (const auto& x : xs) {
       if (x.dst_rank != rank_ || x.src_rank == rank_) continue;
       const void* src = nullptr;
@@ -51,6 +64,7 @@ class PhantomComm final : public Comm {
         if (y.src_rank == rank_ && y.bytes == x.bytes) src = y.src;
       if (src) be.copy(x.dst, src, x.bytes, CopyKind::D2D, s);
     }
+    if (overlap_ && wire > 0) be.delay_since(slot_, wire, s, blocks);
   }
   void allreduce(void*, std::size_t, RedType, RedOp, Backend& be, StreamId s) override {
     if (ar_us_ > 0) be.delay(ar_us_, s, ar_channels_);
@@ -63,6 +77,9 @@ class PhantomComm final : public Comm {
   int rank_, size_;
   double gbps_, ar_us_;
   int channels_, ar_channels_;
+  bool overlap_;
+  Backend* be_ = nullptr;  // owner of slot_ (outlives the communicator, ~Solver)
+  void* slot_ = nullptr;   // device clock stamp of the exchange in flight
 };
 
 }  // namespace

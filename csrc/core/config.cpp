@@ -134,6 +134,7 @@ std::string Config::usage() {
      << "  --fake-allreduce-us U     diagnostic: emulated all-reduce latency for virtual ranks\n"
      << "  --phantom-gbps G --phantom-allreduce-us U --phantom-channels C --phantom-allreduce-channels C\n"
      << "                            phantom-rank proxy (tools/rank_proxy.py) link emulation\n"
+     << "  --phantom-wire serial|overlap  phantom exchange: wire time then copies, or copies inside it\n"
      << "  --quiet                   suppress the banner\n";
   return os.str();
 }
@@ -273,6 +274,11 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--watchdog") c.watchdog_s = to_f64(get("--watchdog"), "--watchdog");
     else if (key == "--fake-allreduce-us") c.fake_allreduce_us = to_f64(get("--fake-allreduce-us"), "--fake-allreduce-us");
     else if (key == "--phantom-gbps") c.phantom_gbps = to_f64(get("--phantom-gbps"), "--phantom-gbps");
+    else if (key == "--phantom-wire") {
+      const std::string v = get("--phantom-wire");
+      if (v != "serial" && v != "overlap") throw UsageError("--phantom-wire serial|overlap");
+      c.phantom_overlap = v == "overlap";
+    }
     else if (key == "--phantom-allreduce-us")
       c.phantom_allreduce_us = to_f64(get("--phantom-allreduce-us"), "--phantom-allreduce-us");
     else if (key == "--phantom-channels") c.phantom_channels = (int)to_i64(get("--phantom-channels"), "--phantom-channels");

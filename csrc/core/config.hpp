@@ -102,6 +102,7 @@ struct Config {
   double phantom_allreduce_us = 20;
   int phantom_channels = 4;       // workgroups an emulated transfer holds per peer
   int phantom_allreduce_channels = 2;
+  bool phantom_overlap = false;   // --phantom-wire overlap: copies inside the emulated wire time
 
   // Parse argv.  Throws UsageError on a malformed command line.
   static Config parse(int argc, const char* const* argv);

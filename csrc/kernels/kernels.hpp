@@ -133,6 +133,8 @@ void check_convergence(DeviceState* s, int slot, void* stream, int count = 1);
 // kernel of `blocks` one-wave workgroups spinning for `us` microseconds on the
 // 100 MHz real-time clock (each holds a wave slot of one CU while it spins)
 void delay(double us, void* stream, int blocks = 1);
+void stamp(void* slot, void* stream);
+void delay_since(const void* slot, double us, void* stream, int blocks = 1);
 // placement probe: out[b] = XCC << 8 | SE/SH/CU id of workgroup b (blocks x 64 threads)
 void cu_probe(unsigned* out, int blocks, double us, void* stream);
 // Adds Σ|T - y| and the point count over `box` into s->error_sum/error_count.

@@ -783,6 +783,28 @@ void delay(double us, void* stream, int blocks) {
   HIPK_CHECK(hipGetLastError());
 }
 
+// phantom transfers whose copies overlap the wire time: one lane stores the
+// 100 MHz clock (a vector store), the delay spins until `ticks` after it
+__global__ void stamp_kernel(unsigned long long* slot) {
+  if (threadIdx.x == 0) *slot = __builtin_amdgcn_s_memrealtime();
+}
+__global__ void delay_since_kernel(const unsigned long long* slot, unsigned long long ticks) {
+  const unsigned long long t0 = *static_cast<const volatile unsigned long long*>(slot);
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void stamp(void* slot, void* stream) {
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, S(stream), static_cast<unsigned long long*>(slot));
+  HIPK_CHECK(hipGetLastError());
+}
+
+void delay_since(const void* slot, double us, void* stream, int blocks) {
+  if (us <= 0) return;
+  hipLaunchKernelGGL(delay_since_kernel, dim3((unsigned)std::max(1, blocks)), dim3(64), 0, S(stream),
+                     static_cast<const unsigned long long*>(slot), (unsigned long long)(us * 100.0));
+  HIPK_CHECK(hipGetLastError());
+}
+
 // ---- error vs analytic steady state T = y -------------------------------------
 constexpr int kErrBlocks = 1024;
 int64_t error_scratch_elems() { return kErrBlocks; }

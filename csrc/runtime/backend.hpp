@@ -101,6 +101,10 @@ class Backend {
   // diagnostic: occupy stream s for `us` microseconds with `blocks` spinning
   // workgroups (emulated collective latency / transfer time); no-op on the CPU
   virtual void delay(double /*us*/, StreamId /*s*/, int /*blocks*/ = 1) {}
+  // device clock stamp into *slot (8 bytes of device memory), and a delay
+  // that ends `us` after the stamp (emulated transfers overlapping copies)
+  virtual void stamp(void* /*slot*/, StreamId /*s*/) {}
+  virtual void delay_since(const void* /*slot*/, double us, StreamId s, int blocks = 1) { delay(us, s, blocks); }
   // tracing ranges (roctx on HIP)
   virtual void range_push(const char* /*name*/) {}
   virtual void range_pop() {}

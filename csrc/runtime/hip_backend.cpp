@@ -292,6 +292,10 @@ class HipBackend final : public Backend {
     op(s, [&](hipStream_t st) { hip::copy_box(t, src, Ls, bs, dst, Ld, bd, st); });
   }
   void delay(double us, StreamId s, int blocks) override { op(s, [&](hipStream_t st) { hip::delay(us, st, blocks); }); }
+  void stamp(void* slot, StreamId s) override { op(s, [&](hipStream_t st) { hip::stamp(slot, st); }); }
+  void delay_since(const void* slot, double us, StreamId s, int blocks) override {
+    op(s, [&](hipStream_t st) { hip::delay_since(slot, us, st, blocks); });
+  }
   void check_convergence(DeviceState* st, int slot, StreamId s, int count) override {
     op(s, [&](hipStream_t q) { hip::check_convergence(st, slot, q, count); });
   }

@@ -52,13 +52,16 @@ def test_cli_two_processes_one_gpu(heat3d_bin, gpu, tmp_path):
     assert (tmp_path / "output" / "out.dat").read_text().count("ZONE") == 2
 
 
-@pytest.mark.parametrize("rank,size,decomp", [(1, 4, (4, 1, 1)), (5, 8, (2, 2, 2))])
-def test_phantom_rank_gpu(h3d, gpu, rank, size, decomp):
+@pytest.mark.parametrize("rank,size,decomp,wire", [(1, 4, (4, 1, 1), "serial"), (5, 8, (2, 2, 2), "serial"),
+                                                   (1, 4, (4, 1, 1), "overlap")])
+def test_phantom_rank_gpu(h3d, gpu, rank, size, decomp, wire):
     """PhantomComm on the GPU (tools/rank_proxy.py): one rank's full overlapped
-    schedule with emulated halo delay kernels; every issued iteration checked."""
+    schedule with emulated halo delay kernels (after the stand-in copies, or
+    ending a wire time after a device clock stamp taken before them);
+    every issued iteration checked."""
     s = h3d.HeatSolver((97, 97, 97), 1 << 40, 0.0, backend="hip", device=0, decomp=decomp,
                        phantom=(rank, size), extra_args=["--temporal", "3", "--phantom-gbps", "50",
-                                                         "--phantom-allreduce-us", "5"])
+                                                         "--phantom-allreduce-us", "5", "--phantom-wire", wire])
     assert s.native.comm_name == "phantom"
     s.initialize()
     s.step(40)

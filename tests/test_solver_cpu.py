@@ -165,7 +165,8 @@ def test_phantom_rank_proxy_runs(h3d, rank, size, decomp, temporal):
     process builds only its subdomain and runs its whole schedule, every
     issued iteration accounted for, nothing converges at eps 0."""
     s = h3d.HeatSolver((20, 20, 20), 1 << 40, 0.0, backend="cpu", decomp=decomp, phantom=(rank, size),
-                       threads=2, extra_args=["--temporal", temporal, "--phantom-allreduce-us", "0"])
+                       threads=2, extra_args=["--temporal", temporal, "--phantom-allreduce-us", "0",
+                                              "--phantom-wire", "overlap" if rank % 2 else "serial"])
     assert s.native.comm_name == "phantom"
     s.initialize()
     s.step(13)

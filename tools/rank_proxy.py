@@ -35,6 +35,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--gbps", type=float, default=50.0, help="emulated halo bandwidth per peer (GB/s)")
     ap.add_argument("--ar-us", type=float, default=20.0, help="emulated all-reduce latency (us)")
+    ap.add_argument("--wire", default="serial", choices=["serial", "overlap"],
+                    help="serial: an exchange is bytes / gbps, then the stand-in D2D copies; overlap: the "
+                         "copies run inside the wire time (a transport moving data while on the wire)")
     ap.add_argument("--backend", default="hip")
     ap.add_argument("--extra", default="", help="extra solver flags, e.g. '--no-overlap'")
     ap.add_argument("--preheat-ms", type=float, default=0.0,
@@ -64,7 +67,8 @@ def main() -> int:
     gb = lambda b: None if b is None else round(b / 1e9, 2)
     s = HeatSolver(N, iter_max=1 << 40, eps=0.0, dtype=args.dtype, backend=args.backend, decomp=dims,
                    device=0 if args.backend == "hip" else None, phantom=(r, P),
-                   extra_args=["--phantom-gbps", str(args.gbps), "--phantom-allreduce-us", str(args.ar_us)]
+                   extra_args=["--phantom-gbps", str(args.gbps), "--phantom-allreduce-us", str(args.ar_us),
+                               "--phantom-wire", args.wire]
                    + (args.extra.split() if args.extra else []))
     if args.trace_schedule:
         os.environ["HEAT3D_TRACE"] = "1"
@@ -92,7 +96,7 @@ def main() -> int:
     # the schedule's phases per sweep (after the timed window, as bench.py's 'phases')
     phases = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in s.native.profile_sweeps(8).items()}
     out = {"proxy": "phantom rank", "rank": r, "ranks": P, "dims": list(dims), "grid": args.grid,
-           "dtype": args.dtype, "gbps": args.gbps, "ar_us": args.ar_us, "extra": args.extra,
+           "dtype": args.dtype, "gbps": args.gbps, "wire": args.wire, "ar_us": args.ar_us, "extra": args.extra,
            "steps": args.steps, "warmup": args.warmup, "preheat_sweeps": preheat,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "kernel": s.kernel,
            "reserved_cus": s.native.reserved_cus, "graph_launches": s.native.graph_launches,
