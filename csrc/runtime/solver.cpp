@@ -1070,6 +1070,14 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   last_bnd_ = lb ? K_ + 1 : K_;
   const StreamId sb = bnd_stream();
   auto boundary_boxes = [&](Local& l) -> const std::vector<Box>& { return lb ? l.tb_boundary_long : l.tb_boundary; };
+  // thin x-slab boundary pieces keep the y-marching thin-slab tiles whatever
+  // tile shape --kernel2 gives the interior (the shape fields pick the form)
+  auto bspec = [&](const Box& b) {
+    if (b.extent(0) > Kp + 1) return ks;
+    KernelSpec t = ks;
+    t.V = t.R = t.WZ = t.WY = t.NT = t.L = t.ZS = 0;
+    return t;
+  };
   if (hch_ <= 1) {
     enqueue_halo(bi, kComm, dv);
   } else {
@@ -1088,7 +1096,7 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
         for (Box b : boundary_boxes(l)) {
           b.lo[1] = std::max(b.lo[1], ych_[c]);
           b.hi[1] = std::min(b.hi[1], ych_[c + 1]);
-          if (!b.empty()) be_->sweep(dt_, params(l, b), ks, sb);
+          if (!b.empty()) be_->sweep(dt_, params(l, b), bspec(b), sb);
         }
       ev_record(EV_BCH + c, sb);
     };
@@ -1168,7 +1176,7 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
     be_->range_push("boundary");
     prof_record(prof_idx_, PE_BND0, kComm);
     for (auto& l : local_)
-      for (const Box& b : boundary_boxes(l)) be_->sweep(dt_, params(l, b), ks, kComm);
+      for (const Box& b : boundary_boxes(l)) be_->sweep(dt_, params(l, b), bspec(b), kComm);
     prof_record(prof_idx_, PE_BND1, kComm);
     be_->range_pop();
     ev_record(EV_BND + q, kComm);
