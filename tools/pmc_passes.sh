@@ -3,12 +3,13 @@
 # its own hard time limit; counter-slot limits of gfx950 respected: <= 8 SQ,
 # <= 4 TCC, <= 2 TA per pass).  Counters are per dispatch: every row of the
 # summary is one 1024^3 sweep (tools/summarize_rocprof.py takes the median).
-# Usage: tools/pmc_passes.sh OUTDIR VARIANT [N] [DTYPE]
+# Usage: tools/pmc_passes.sh OUTDIR VARIANT [N] [DTYPE] [SET]
+#   SET = default (issue, LDS, L2 / HBM bytes) | latency (L1 / TLB stalls, L2 read latency, TA / TD)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 ROOT=$(pwd)
-out=$1; var=$2; n=${3:-1024}; dt=${4:-fp64}
+out=$1; var=$2; n=${3:-1024}; dt=${4:-fp64}; set=${5:-default}
 case "$out" in /*) ;; *) out="$ROOT/$out" ;; esac
 mkdir -p "$out"
 passes=(
@@ -19,6 +20,13 @@ passes=(
   "FETCH_SIZE"
   "WRITE_SIZE"
 )
+if [ "$set" = latency ]; then
+  passes=(
+    "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_THRASHING_STALL_sum GRBM_GUI_ACTIVE"
+    "TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_UTCL1_SERIALIZATION_STALL_sum"
+    "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum SQ_WAVE_CYCLES SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM"
+  )
+fi
 i=0
 for p in "${passes[@]}"; do
   timeout -s KILL 90 rocprofv3 --pmc $p -d "$out/p$i" -o run --output-format csv -- \
