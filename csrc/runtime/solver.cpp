@@ -639,7 +639,15 @@ void Solver::calibrate_remainders() {
     kl.K = K_ + 1;
     if (!hip::lean_supported(dt_, kl)) return;
   }
-  Event e0 = be_->event_create(), e1 = be_->event_create();
+  struct Events {  // released on every exit (a refused kernel variant throws)
+    Backend* be;
+    Event a, b;
+    ~Events() {
+      be->event_destroy(a);
+      be->event_destroy(b);
+    }
+  } ev{be_.get(), be_->event_create(), be_->event_create()};
+  Event e0 = ev.a, e1 = ev.b;
   // Kp = 1: a single step of the owned box; else a sweep of depth Kp
   auto launch = [&](int Kp, const KernelSpec& ks) {
     for (auto& l : local_) {
@@ -712,8 +720,6 @@ void Solver::calibrate_remainders() {
       be_->sync(kCompute);
       best[c] = std::min(best[c], (double)be_->elapsed_ms(e0, e1) / reps);
     }
-  be_->event_destroy(e0);
-  be_->event_destroy(e1);
   // per depth: the fastest candidate (a rank-local kernel choice: the halo
   // of a partial sweep does not depend on its tile shape)
   std::vector<double> cost(K_ + 2, 1e30);
