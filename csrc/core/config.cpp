@@ -108,6 +108,8 @@ std::string Config::usage() {
      << "  --progress S              stderr heartbeat (iteration, residual, rate) every S seconds of run()\n"
      << "  --time-limit S            run(): stop (not converged) after about S seconds (0 = no limit)\n"
      << "  --threads N               CPU backend OpenMP threads\n"
+     << "  --thin-layers             overlapped block sweeps: K-thick y / z boundary layers (default: one\n"
+     << "                            tile stride thick, so that their tiles are not mostly halo)\n"
      << "  --halo-chunks M           overlapped x-slab sweeps: halo in M row chunks, each chunk's boundary\n"
      << "                            slabs start once it has landed (0 auto, 1 off, <= 8)\n"
      << "  --reserve-cus N           CUs kept free of the interior sweep for comm / boundary / check\n"
@@ -243,6 +245,7 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--no-long-sweeps") c.long_sweeps = 0;
     else if (key == "--no-core-rim") c.core_rim = false;
     else if (key == "--core-rim") c.core_rim = true;
+    else if (key == "--thin-layers") c.tile_layers = false;
     else if (key == "--halo-chunks") {
       c.halo_chunks = (int)to_i64(get("--halo-chunks"), "--halo-chunks");
       if (c.halo_chunks < 0 || c.halo_chunks > 8) throw UsageError("--halo-chunks takes 0 (auto) .. 8");

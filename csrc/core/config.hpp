@@ -72,6 +72,9 @@ struct Config {
   // boundary slabs of each chunk start as soon as it (and the next) landed,
   // on their own stream (0 = auto, 1 = one piece)
   int halo_chunks = 0;
+  // overlapped block sweeps: y / z boundary layers one tile stride thick
+  // (whole tiles instead of K-thin ones; --thin-layers: K thick)
+  bool tile_layers = true;
   bool core_rim = false;          // overlapped sweeps: interior as a core (not waiting for the previous
                                   // boundary slabs) and a rim (waiting for them); measured slower
                                   // in the 8-GPU proxy (profiles/rank_proxy_r04.md), opt-in

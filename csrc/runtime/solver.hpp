@@ -131,6 +131,15 @@ class Solver {
   std::array<int64_t, 3> ghost_depth() const { return {hd_[0], hd_[1], hd_[2]}; }
   bool long_halo_sweeps() const { return long_halo_; }
   int halo_chunks() const { return hch_; }
+  // the overlapped sweeps' interior and boundary pieces of local subdomain i
+  // (lo0, hi0, lo1, hi1, lo2, hi2 each)
+  std::vector<std::array<int64_t, 6>> sweep_pieces(int i) const {
+    std::vector<std::array<int64_t, 6>> out;
+    auto add = [&](const Box& b) { out.push_back({b.lo[0], b.hi[0], b.lo[1], b.hi[1], b.lo[2], b.hi[2]}); };
+    add(local_.at(i).tb_interior);
+    for (const Box& b : local_.at(i).tb_boundary) add(b);
+    return out;
+  }
   // remainder policy: which n mod K run as long sweeps, and the start-up
   // sweep timings that decided it (empty when not measured)
   unsigned long_remainders() const { return long_rem_; }

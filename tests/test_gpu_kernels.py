@@ -92,6 +92,29 @@ def test_init_field_matches_cpu(h3d, gpu):
         assert torch.equal(c.flat, d.flat.cpu())
 
 
+@pytest.mark.parametrize("box", [[0, 6, 0, 9, 0, 1], [0, 6, 0, 9, 67, 70], [0, 6, -1, 10, -1, 2],
+                                 [1, 5, 2, 7, 10, 27], [0, 6, 0, 9, 0, 70], [0, 1, 0, 9, 0, 70]])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_pack_unpack_box_shapes(h3d, gpu, box, dtype):
+    """Pack / unpack of thin z faces (1-3 columns: many rows per workgroup),
+    ghost-inclusive and general boxes, against plain tensor slicing."""
+    ops = h3d.ops
+    n = (6, 9, 70)
+    _, dev = _random_field(ops, n, dtype, gpu, seed=7)
+    ex, ey, ez = box[1] - box[0], box[3] - box[2], box[5] - box[4]
+    buf = torch.empty(ex * ey * ez, dtype=dtype, device=gpu)
+    ops.pack_box(dev, box, buf)
+    g = dev.ghosted()
+    want = g[box[0] + 1:box[1] + 1, box[2] + 1:box[3] + 1, box[4] + 1:box[5] + 1]
+    torch.cuda.synchronize()
+    assert torch.equal(buf.view(ex, ey, ez).cpu(), want.cpu())
+    other = ops.PaddedField(n, dtype=dtype, device=gpu)
+    ops.unpack_box(other, box, buf)
+    torch.cuda.synchronize()
+    got = other.ghosted()[box[0] + 1:box[1] + 1, box[2] + 1:box[3] + 1, box[4] + 1:box[5] + 1]
+    assert torch.equal(got.cpu(), want.cpu())
+
+
 def test_pack_unpack_roundtrip(h3d, gpu):
     ops = h3d.ops
     n = (6, 9, 70)

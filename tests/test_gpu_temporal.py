@@ -543,6 +543,27 @@ def test_chunked_halo_pipeline_gpu(h3d, gpu, vr, M, dtype):
     assert a.native.verify_halos() == 0
 
 
+@pytest.mark.parametrize("vr,dims,n", [(8, (2, 2, 2), (82, 180, 260)), (4, (1, 2, 2), (40, 180, 380)),
+                                        (4, (2, 2, 1), (90, 180, 100))])
+@pytest.mark.parametrize("dtype,thin", [("fp64", False), ("fp32", False), ("fp64", True)])
+def test_tile_thick_block_layers_gpu(h3d, gpu, vr, dims, n, dtype, thin):
+    """Overlapped block sweeps with y / z boundary layers one tile stride
+    thick (whole tiles; --thin-layers: K thick) on the device streams:
+    regular, partial and long sweeps bitwise equal to single steps."""
+    extra = ["--long-sweeps", "on"] + (["--thin-layers"] if thin else [])
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims, extra_args=extra)
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
+    a.initialize(), b.initialize()
+    for k in (5, 20, 11, 4):
+        a.step(k)
+        b.step(k)
+        a.synchronize(), b.synchronize()
+        sa, sb = a.native.state(), b.native.state()
+        assert sa["iter"] == sb["iter"] and sa["last_residual"] == sb["last_residual"]
+        assert np.array_equal(a.gather(), b.gather()), (vr, dims, dtype, thin, k)
+    assert a.native.verify_halos() == 0
+
+
 @pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (2, 2, 2))])
 def test_long_sweep_across_halos_rollback_gpu(h3d, gpu, vr, dims):
     n = (33, 33, 33)

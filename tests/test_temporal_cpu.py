@@ -431,6 +431,28 @@ def test_chunked_halo_pipeline(h3d, vr, dims, K, M):
     assert a.native.verify_halos() == 0
 
 
+@pytest.mark.parametrize("thin", [False, True])
+def test_tile_thick_block_layers(h3d, thin):
+    """Overlapped block sweeps: y / z boundary layers one tile stride thick
+    (42 rows, 58 columns at fp64 K = 3) where the subdomain has room, K thin
+    with --thin-layers or without room; the pieces tile the owned box and the
+    sweeps stay bitwise equal to single steps."""
+    n = (14, 172, 236)   # 2x2 in y, z: owned 85 x 117 per rank
+    extra = ["--temporal", "3"] + (["--thin-layers"] if thin else [])
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", virtual_ranks=4, decomp=(1, 2, 2), extra_args=extra)
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", extra_args=T1)
+    pieces = [list(p) for p in a.native.sweep_pieces(0)]   # rank 0: neighbours above in y and z
+    ty, tz = (3, 3) if thin else (42, 58)
+    assert pieces == [[0, 12, 0, 85 - ty, 0, 117 - tz],            # interior
+                      [0, 12, 85 - ty, 85, 0, 117],                # y layer (full z)
+                      [0, 12, 0, 85 - ty, 117 - tz, 117]], pieces  # z layer (interior y)
+    a.initialize(), b.initialize()
+    for k in (7, 6, 3):
+        a.step(k)
+        b.step(k)
+        assert np.array_equal(a.gather(), b.gather()), (thin, k)
+
+
 def test_chunked_halo_fallbacks(h3d):
     """Bands need x faces only, the lagged check and >= K + 3 rows each: block
     decompositions, thin slabs and --halo-chunks 1 run the single exchange."""
