@@ -108,6 +108,8 @@ std::string Config::usage() {
      << "  --progress S              stderr heartbeat (iteration, residual, rate) every S seconds of run()\n"
      << "  --time-limit S            run(): stop (not converged) after about S seconds (0 = no limit)\n"
      << "  --threads N               CPU backend OpenMP threads\n"
+     << "  --boundary-stream auto|comm|compute  overlapped sweeps: boundary pieces beside the interior (comm\n"
+     << "                            stream, behind the halo) or after it on the compute stream\n"
      << "  --thin-layers             overlapped block sweeps: K-thick y / z boundary layers (default: one\n"
      << "                            tile stride thick, so that their tiles are not mostly halo)\n"
      << "  --halo-chunks M           overlapped x-slab sweeps: halo in M row chunks, each chunk's boundary\n"
@@ -246,6 +248,13 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--no-core-rim") c.core_rim = false;
     else if (key == "--core-rim") c.core_rim = true;
     else if (key == "--thin-layers") c.tile_layers = false;
+    else if (key == "--boundary-stream") {
+      const std::string v = get("--boundary-stream");
+      if (v == "auto") c.boundary_stream = -1;
+      else if (v == "comm") c.boundary_stream = 0;
+      else if (v == "compute") c.boundary_stream = 1;
+      else throw UsageError("--boundary-stream auto|comm|compute");
+    }
     else if (key == "--halo-chunks") {
       c.halo_chunks = (int)to_i64(get("--halo-chunks"), "--halo-chunks");
       if (c.halo_chunks < 0 || c.halo_chunks > 8) throw UsageError("--halo-chunks takes 0 (auto) .. 8");

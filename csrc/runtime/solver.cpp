@@ -363,6 +363,9 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
       for (int c = 0; c <= hch_ && hch_ > 1; ++c) ych_.push_back(ny * c / hch_);
     }
   }
+  // boundary pieces on the compute stream, after the interior: explicit only
+  // for now (auto = the comm stream)
+  bcomp_ = tb_overlap_ && hch_ <= 1 && cfg_.boundary_stream == 1;
   dstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
   hstate_ = static_cast<DeviceState*>(be_->alloc_host(2 * sizeof(DeviceState)));
   std::memset(hstate_, 0, 2 * sizeof(DeviceState));
@@ -1102,7 +1105,11 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
     return t;
   };
   if (hch_ <= 1) {
+    // (boundary pieces on the compute stream: the halo sends what the
+    // previous ones wrote there; EV_HCH + 0 marks the halo landed)
+    if (bcomp_) ev_wait(kComm, EV_BND + (q ^ 1));
     enqueue_halo(bi, kComm, dv);
+    if (bcomp_) ev_record(EV_HCH, kComm);
   } else {
     // [B1+B2] chunked: band c of the halo, then (boundary stream) the boundary
     // slabs of band c-1, whose Kp-step cone reaches Kp rows into band c.
@@ -1150,7 +1157,7 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   ev_wait(kCompute, EV_CHK + chk_prev);
   be_->range_push("interior");
   prof_record(prof_idx_, PE_INT0, kCompute);
-  bool split = prev_bnd > 0 && cfg_.core_rim;
+  bool split = prev_bnd > 0 && cfg_.core_rim && !bcomp_;
   std::vector<std::pair<Box, std::vector<Box>>> parts;  // per local: core, rim pieces
   for (auto& l : local_) {
     const Box& ib = lb ? l.tb_interior_long : l.tb_interior;
@@ -1193,16 +1200,21 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
   if (hch_ <= 1) {
-    // [B2] the boundary slabs, behind the halo on the comm stream
-    ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
-    ev_wait(kComm, EV_CHK + chk_prev);
+    // [B2] the boundary slabs, behind the halo on the comm stream (or behind
+    // the interior and the halo on the compute stream)
+    if (bcomp_) {
+      ev_wait(kCompute, EV_HCH);
+    } else {
+      ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
+      ev_wait(kComm, EV_CHK + chk_prev);
+    }
     be_->range_push("boundary");
-    prof_record(prof_idx_, PE_BND0, kComm);
+    prof_record(prof_idx_, PE_BND0, sb);
     for (auto& l : local_)
-      for (const Box& b : boundary_boxes(l)) be_->sweep(dt_, params(l, b), bspec(b), kComm);
-    prof_record(prof_idx_, PE_BND1, kComm);
+      for (const Box& b : boundary_boxes(l)) be_->sweep(dt_, params(l, b), bspec(b), sb);
+    prof_record(prof_idx_, PE_BND1, sb);
     be_->range_pop();
-    ev_record(EV_BND + q, kComm);
+    ev_record(EV_BND + q, sb);
   }
   // [C] all residuals, all checks: now, or (ordered collectives) after the
   // next sweep's halo.  With the lag nothing waits for CHK(q) before sweep

@@ -131,6 +131,7 @@ class Solver {
   std::array<int64_t, 3> ghost_depth() const { return {hd_[0], hd_[1], hd_[2]}; }
   bool long_halo_sweeps() const { return long_halo_; }
   int halo_chunks() const { return hch_; }
+  int boundary_on_compute() const { return bcomp_ ? 1 : 0; }
   // the overlapped sweeps' interior and boundary pieces of local subdomain i
   // (lo0, hi0, lo1, hi1, lo2, hi2 each)
   std::vector<std::array<int64_t, 6>> sweep_pieces(int i) const {
@@ -315,7 +316,9 @@ class Solver {
   int hch_ = 1;
   std::vector<int64_t> ych_;
   StreamId red_stream() const { return hch_ > 1 && chain_ ? kComm : kReduce; }
-  StreamId bnd_stream() const { return hch_ > 1 ? kReduce : kComm; }
+  StreamId bnd_stream() const { return hch_ > 1 ? kReduce : bcomp_ ? kCompute : kComm; }
+  // boundary pieces after the interior on the compute stream (--boundary-stream)
+  bool bcomp_ = false;
   bool ordered_halo_ = false; // axis-ordered exchange filling edges / corners (deep y / z halos)
   int last_kind_ = 0;         // 1 = single step, 2 = pair: last enqueued schedule
   DType dt_;

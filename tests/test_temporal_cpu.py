@@ -431,6 +431,24 @@ def test_chunked_halo_pipeline(h3d, vr, dims, K, M):
     assert a.native.verify_halos() == 0
 
 
+@pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (2, 2, 2)), (4, (1, 2, 2))])
+@pytest.mark.parametrize("K", [2, 3])
+def test_boundary_on_compute_stream(h3d, vr, dims, K):
+    """--boundary-stream compute: the boundary pieces after the interior on
+    the compute stream (the halo waits for the previous ones there); regular,
+    partial and long sweeps bitwise equal to single steps."""
+    n = (33, 29, 31)
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", virtual_ranks=vr, decomp=dims,
+                       extra_args=["--temporal", str(K), "--boundary-stream", "compute"])
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", extra_args=T1)
+    assert a.native.boundary_on_compute == 1
+    a.initialize(), b.initialize()
+    for k in (5, 20, 7, 11, 4):
+        a.step(k)
+        b.step(k)
+        assert np.array_equal(a.gather(), b.gather()), (vr, dims, K, k)
+
+
 @pytest.mark.parametrize("thin", [False, True])
 def test_tile_thick_block_layers(h3d, thin):
     """Overlapped block sweeps: y / z boundary layers one tile stride thick
