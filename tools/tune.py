@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--probes", action="store_true", help="also run the HBM copy/read probes")
+    ap.add_argument("--check", action="store_true",
+                    help="before timing: one sweep of every variant from the same field must equal the first "
+                         "variant's, bit for bit (variants with equal steps per sweep)")
     a = ap.parse_args()
 
     import torch
@@ -69,6 +72,24 @@ def main():
             print(json.dumps({"variant": v, "skipped": str(e)[:160]}), flush=True)
     a.variants = ok
     torch.cuda.synchronize()
+    if a.check and a.variants:
+        f2 = ops.PaddedField(n, dtype=dt, device=dev)
+        ops.init_field(f2, (1, 1, 1), N, h)
+        ref = None
+        for v in a.variants:
+            f2.owned().zero_()
+            run(v, f0, f2)
+            torch.cuda.synchronize()
+            got = f2.owned().clone()
+            if ref is None:
+                ref, ref_v = got, v
+                continue
+            same = steps(v) == steps(ref_v)
+            diff = int((got != ref).sum().item()) if same else None
+            print(json.dumps({"check": v, "against": ref_v, "differing_points": diff}), flush=True)
+            if same and diff:
+                raise SystemExit(f"tune.py --check: {v} differs from {ref_v} at {diff} points")
+        del f2
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(a.rounds):
         for v in a.variants:
