@@ -112,16 +112,12 @@ std::string Config::usage() {
      << "                            stream, behind the halo) or after it on the compute stream\n"
      << "  --thin-layers             overlapped block sweeps: K-thick y / z boundary layers (default: one\n"
      << "                            tile stride thick, so that their tiles are not mostly halo)\n"
-     << "  --halo-chunks M           overlapped x-slab sweeps: halo in M row chunks, each chunk's boundary\n"
-     << "                            slabs start once it has landed (0 auto, 1 off, <= 8)\n"
      << "  --reserve-cus N           CUs kept free of the interior sweep for comm / boundary / check\n"
      << "                            kernels (default: 8 = one per XCD when the overlapped\n"
      << "                            multi-rank schedule runs, else 0)\n"
      << "  --lag auto|on|off         lagged convergence check of overlapped sweeps (3rd field buffer)\n"
      << "  --no-block-overlap        block decompositions: exchange the halo first, then sweep\n"
      << "  --no-long-sweeps          step-count remainders as partial sweeps, not K+1-step sweeps\n"
-     << "  --core-rim                overlapped sweeps: interior as a core that does not wait for the previous\n"
-     << "                            boundary slabs plus a rim that does (opt-in; --no-core-rim: off, default)\n"
      << "  --long-sweeps auto|on|off remainders as K+1-step sweeps: auto = where the start-up timing of\n"
      << "                            the sweeps finds them cheaper than a partial sweep (default auto;\n"
      << "                            GPU only, measure = on any backend)\n"
@@ -245,8 +241,9 @@ Config Config::parse(int argc, const char* const* argv) {
     }
     else if (key == "--no-block-overlap") c.block_overlap = false;
     else if (key == "--no-long-sweeps") c.long_sweeps = 0;
-    else if (key == "--no-core-rim") c.core_rim = false;
-    else if (key == "--core-rim") c.core_rim = true;
+    else if (key == "--core-rim" || key == "--no-core-rim" || key == "--halo-chunks")
+      throw UsageError(key + " was retired in round 5 (measured slower on every configuration, "
+                             "profiles/rank_proxy_r04.md)");
     else if (key == "--thin-layers") c.tile_layers = false;
     else if (key == "--boundary-stream") {
       const std::string v = get("--boundary-stream");
@@ -254,10 +251,6 @@ Config Config::parse(int argc, const char* const* argv) {
       else if (v == "comm") c.boundary_stream = 0;
       else if (v == "compute") c.boundary_stream = 1;
       else throw UsageError("--boundary-stream auto|comm|compute");
-    }
-    else if (key == "--halo-chunks") {
-      c.halo_chunks = (int)to_i64(get("--halo-chunks"), "--halo-chunks");
-      if (c.halo_chunks < 0 || c.halo_chunks > 8) throw UsageError("--halo-chunks takes 0 (auto) .. 8");
     }
     else if (key == "--long-sweeps") {
       const std::string v = get("--long-sweeps");

@@ -68,10 +68,6 @@ struct Config {
   int verbose = 0;
   double progress_s = 0;          // run(): stderr heartbeat period (0 = off)
   double time_limit_s = 0;        // run(): wall budget, stop unconverged past it (0 = none)
-  // overlapped x-slab sweeps: the halo travels in M row chunks and the
-  // boundary slabs of each chunk start as soon as it (and the next) landed,
-  // on their own stream (0 = auto, 1 = one piece)
-  int halo_chunks = 0;
   // overlapped block sweeps: y / z boundary layers one tile stride thick
   // (whole tiles instead of K-thin ones; --thin-layers: K thick)
   bool tile_layers = true;
@@ -80,9 +76,6 @@ struct Config {
   // the compute stream (no contention for CUs; the halo still overlaps the
   // interior).  -1 auto
   int boundary_stream = -1;       // -1 auto, 0 comm, 1 compute
-  bool core_rim = false;          // overlapped sweeps: interior as a core (not waiting for the previous
-                                  // boundary slabs) and a rim (waiting for them); measured slower
-                                  // in the 8-GPU proxy (profiles/rank_proxy_r04.md), opt-in
   bool quiet = false;
   int cpu_threads = 0;
   int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules

@@ -170,9 +170,6 @@ XPlan fixed_xplan(int64_t nx, int64_t tiles, int seg);
 double xplan_makespan(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fill, int U);
 // A tiling's sweep cost for the z-stride choice: max(makespan, work / HBM-saturating slots)
 double tiling_cost(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fill, int U);
-// Same model for the persistent walk: `live` workgroups, each a contiguous
-// 1/live of the tile-major (tile, plane) list, a fill per tile it touches.
-double walk_makespan(int64_t nx, int64_t tiles, int live, int fill, int U);
 // Compute units of the current device (cached per device).
 int device_cus();
 

@@ -250,16 +250,6 @@ int device_cus() {
   return std::max(1, cus);
 }
 
-double walk_makespan(int64_t nx, int64_t tiles, int live, int fill, int U) {
-  // the longest range: ceil(W / live) plane steps over at most
-  // 1 + ceil(range / nx) pieces, each with its fill and its last unrolled
-  // chunk half empty on average, plus a residual commit (~2 steps) per piece
-  const int64_t W = nx * tiles;
-  const double range = std::ceil((double)W / std::max(1, live));
-  const double pieces = 1.0 + std::ceil(range / (double)std::max<int64_t>(1, nx));
-  return range + pieces * (fill + 0.5 * U + 2.0);
-}
-
 int device_slots(const void* kernel, int block) {
   int dev = 0, cus = 256, per = 1, lds_cu = 160 * 1024;
   if (hipGetDevice(&dev) == hipSuccess) {

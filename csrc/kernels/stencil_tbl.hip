@@ -13,8 +13,8 @@ namespace heat3d {
 namespace hip {
 
 // every variant dispatch_tbl can launch, instantiated elsewhere
-#define H3D_V(T, R, WY, K, Q, N, S, W, P) \
-  extern template void launch_tbl<T, R, WY, K, Q, N, S, W>(const StencilParams&, const KernelSpec&, hipStream_t);
+#define H3D_V(T, R, WY, K, Q, N, S, P) \
+  extern template void launch_tbl<T, R, WY, K, Q, N, S>(const StencilParams&, const KernelSpec&, hipStream_t);
 #include "stencil_tbl_variants.inc"
 #undef H3D_V
 
@@ -54,7 +54,6 @@ static int lean_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int esi
   auto cost = [&](int zs) {
     const int64_t tiles = std::max<int64_t>(1, (nz + zs - 1) / zs) * nyb;
     const XPlan p = L > 0 ? fixed_xplan(nx, tiles, L) : plan_x(nx, tiles, slots, 2 * (K - 1), U, L == -1);
-    if (L == -2) return walk_makespan(nx, tiles, slots, 2 * (K - 1), U);
     return tiling_cost(p, nx, tiles, slots, 2 * (K - 1), U);
   };
   constexpr double kAlignedGain = 0.92;
@@ -109,17 +108,16 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
     return true;                                                   \
   }
   // output-store cache-policy bits (spec field 7: 2 = nt, 1 / 16 = sc0 / sc1), default shapes only
-#define H3D_TBLA(RR, YY, KK, AA, WW)                                    \
-  if (R == RR && WY == YY && K == KK && Q == 3 && r.O == (AA)) {        \
-    if (p) launch_tbl<Real, RR, YY, KK, 3, (AA), false, WW>(*p, k, s);  \
-    return true;                                                        \
+#define H3D_TBLA(RR, YY, KK, AA)                                       \
+  if (R == RR && WY == YY && K == KK && Q == 3 && r.O == (AA)) {       \
+    if (p) launch_tbl<Real, RR, YY, KK, 3, (AA), false>(*p, k, s);      \
+    return true;                                                       \
   }
-  // the default shapes carry the persistent-walk form
-  H3D_TBLA(3, 16, 3, 2, true) H3D_TBLA(3, 16, 3, 3, false) H3D_TBLA(3, 16, 3, 17, false)
-  H3D_TBLA(3, 16, 3, 18, false) H3D_TBLA(3, 16, 3, 19, false)
-  H3D_TBLA(2, 16, 4, 2, false) H3D_TBLA(3, 16, 2, 2, false) H3D_TBLA(5, 16, 2, 2, false)
-  H3D_TBLA(3, 12, 4, 2, true)  // the fp64 K = 4 default (long sweeps: 12 waves, 36 rows)
-  H3D_TBLA(4, 12, 4, 2, false)
+  H3D_TBLA(3, 16, 3, 2) H3D_TBLA(3, 16, 3, 3) H3D_TBLA(3, 16, 3, 17)
+  H3D_TBLA(3, 16, 3, 18) H3D_TBLA(3, 16, 3, 19)
+  H3D_TBLA(2, 16, 4, 2) H3D_TBLA(3, 16, 2, 2) H3D_TBLA(5, 16, 2, 2)
+  H3D_TBLA(3, 12, 4, 2)  // the fp64 K = 4 default (long sweeps: 12 waves, 36 rows)
+  H3D_TBLA(4, 12, 4, 2)
 #undef H3D_TBLA
   // 16 waves (<= 128 VGPRs, LDS 2K x 16 KiB): K <= 4; 12 waves (<= 168 VGPRs): K = 5
   H3D_TBL(3, 16, 4, 3) H3D_TBL(3, 16, 4, 4) H3D_TBL(3, 16, 3, 3) H3D_TBL(3, 16, 3, 4)

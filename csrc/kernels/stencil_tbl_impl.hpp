@@ -108,11 +108,8 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 }  // namespace
 
 // NTS: store cache policy; SW: swapped axes (x planes are the tile rows, the
-// kernel marches y): the row neighbours are the x terms of the update; PW:
-// persistent walk (a workgroup loops over several pieces).  PW is its own
-// instantiation: the piece loop costs the single-piece form 8 VGPRs and ~60
-// SGPR spills to VGPR lanes (ROCm 7.2), which the x plan does not need.
-template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false, bool PW = false>
+// kernel marches y): the row neighbours are the x terms of the update.
+template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
 __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ in, Real* __restrict__ out,
                                                        TBLArgs g, Real Dx, Real Dy, Real Dz,
                                                        unsigned long long* res, const int* done) {
@@ -140,22 +137,15 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
   const int zs = g.zs;
   const int ntile = g.nzb * g.nyb;
   const int nxb = g.bhi[0] - g.blo[0];
-  // This workgroup's work: plane steps [w, wend) of the tile-major list
-  // (tile t, plane x) -> t * nxb + x, walked piece by piece (a piece = one
-  // tile's contiguous planes; each pays the 2(K-1)-plane pipeline fill).
-  //   * x plan (rb >= 0): one piece per block, x segments of `seg` planes
-  //     (plan_x: whole rounds of pieces, then a split tail);
-  //   * persistent (PW): exactly as many blocks as the device holds at
-  //     once, each a contiguous 1/n1 of the list, so no round of workgroups
-  //     is left partly empty and a block only pays a fill where its range
-  //     crosses into the next tile.
+  // This workgroup's piece: plane steps [w, wend) of the tile-major list
+  // (tile t, plane x) -> t * nxb + x, one piece per block, x segments of
+  // `seg` planes (plan_x: whole rounds of pieces, then a split tail); each
+  // piece pays the 2(K-1)-plane pipeline fill.  (The persistent walk of round 3,
+  // every block a contiguous 1/n of the list, measured 18-22% slower on
+  // MI355X: the x plan's concurrent workgroups sweep neighbouring tiles over
+  // the same x planes, so their overlapping halo rows are L2 hits.)
   int64_t w, wend;
-  if (PW) {
-    const int64_t W = (int64_t)ntile * nxb;
-    const int e = remap(blk, g.n1);
-    w = (int64_t)e * W / g.n1;
-    wend = (int64_t)(e + 1) * W / g.n1;
-  } else {
+  {
     int pc, part;
     const int rr = g.rb & 0x3fffffff;
     if (blk < g.n1) {
@@ -178,12 +168,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     wend = (int64_t)tt * nxb + xhi_p;
   }
 
-  do {
   // tile order: z fastest
   const int tt = (int)(w / nxb);
   const int xlo_p = (int)(w - (int64_t)tt * nxb);
   const int xhi_p = (int)min((int64_t)nxb, xlo_p + (wend - w));
-  w += xhi_p - xlo_p;
   const int zb = tt % g.nzb, ybk = tt / g.nzb;
 
   const int wave = sgpr(threadIdx.x >> 6);
@@ -370,16 +358,12 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     residual_commit_block<WY, K>(res, mm, nan_seen,
                                  *reinterpret_cast<unsigned long long(*)[WY][K]>(&s_row[0][0][0][0][0]));
   }
-  if (PW && w < wend) __syncthreads();  // the next piece rewrites the exchange buffer
-  } while (PW && w < wend);  // pieces
 }
 
-// WALK: the persistent-walk instantiation exists for this shape (the default
-// shapes); otherwise only the x plan runs
-template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false, bool WALK = false>
+template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
 void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   constexpr bool swap_xy = SW;
-  const void* kfn = reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW, false>);
+  const void* kfn = reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW>);
   Box b = p.box;
   constexpr int TY = WY * R;
   // swap_xy: march along y with x as the tile rows (thin x slabs: a tile of
@@ -441,20 +425,9 @@ void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
     ga.nzb = (int)std::max<int64_t>(1, (b.extent(2) + zs - 1) / zs);
     return (int64_t)ga.nzb * ga.nyb;
   };
-  const int64_t ntiles = set_zs(g, ZS);
+  (void)set_zs(g, ZS);
   const int64_t nxb = b.extent(0);
-  // workgroups the stream can hold at once (CUs kept off it by a CU mask
-  // are not there for the persistent walk)
-  const int cus = device_cus();
-  const int live = std::max(1, (int)((int64_t)slots * std::max(1, cus - p.cu_reserved) / std::max(1, cus)));
-  HEAT3D_CHECK(WALK || ks.L != -2, "tl variant " << ks.str() << " has no persistent-walk form");
-  // The walk is opt-in (L = -2): its makespan model wins on every box here,
-  // but MI355X measures it 18-22% slower than the x plan (1024^3 fp64 677 vs
-  // 822 GLUPS, 128 x 1022^2 563 vs 721, 256 x 1022^2 582 vs 706; round 3).
-  // The x plan's concurrent workgroups sweep neighbouring tiles over the same
-  // x planes, so the overlapping halo columns and rows of a tile are L2 hits;
-  // a walk's workgroups sit at unrelated x offsets of their tiles.
-  const bool walk = WALK && ks.L == -2;
+  HEAT3D_CHECK(ks.L != -2, "tl: the persistent walk (L = -2) was retired in round 5 (18-22% slower than the x plan)");
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl: residual slots " << p.slot << "+" << K);
   auto scratch = [](const void* f) {
     hipFuncAttributes a{};
@@ -465,26 +438,9 @@ void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   HEAT3D_CHECK(spill == 0, "tl variant " << ks.str() << " spills " << spill << " B of registers per lane");
   unsigned long long* r = p.state && p.residual ? &p.state->residual[p.slot] : nullptr;
   const int* done = p.state ? &p.state->done : nullptr;
-  if constexpr (WALK) {
-    if (walk) {
-      g.segsplit = 0;
-      g.n1 = (int)std::min<int64_t>(live, ntiles * nxb);
-      g.rb = -1;
-      static const int spill_w = scratch(reinterpret_cast<const void*>(&stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>));
-      HEAT3D_CHECK(spill_w == 0, "tl walk variant " << ks.str() << " spills " << spill_w << " B per lane");
-      if (trace_enabled())
-        std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: walk tiles=%dx%d blocks=%d\n", K, (long long)nxb,
-                     g.nzb, g.nyb, g.n1);
-      hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, true>), dim3((unsigned)g.n1), dim3(64 * WY), 0, s,
-                         static_cast<const Real*>(p.in), static_cast<Real*>(p.out), g, (Real)p.D[0], (Real)p.D[1],
-                         (Real)p.D[2], r, done);
-      HIPK_CHECK(hipGetLastError());
-      return;
-    }
-  }
-  // spec field L: > 0 fixed segments, -1 equal segments, -2 persistent walk,
-  // -3 the x plan; 0: the schedule timed for this box (tune_schedule: z
-  // stride and x schedule), else the x plan
+  // spec field L: > 0 fixed segments, -1 equal segments, -3 the x plan;
+  // 0: the schedule timed for this box (tune_schedule: z stride and x
+  // schedule), else the x plan
   auto fire = [&](int zs, int Lx) {
     TBLArgs ga = g;
     const int64_t tiles = set_zs(ga, zs);
@@ -499,7 +455,7 @@ void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
       std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: zs=%d L=%d seg=%d tiles=%dx%d blocks=%lld (model %.1f)\n",
                    K, (long long)nxb, zs, Lx, xp.seg, ga.nzb, ga.nyb, (long long)nblocks,
                    xplan_makespan(xp, nxb, tiles, slots, 2 * (K - 1), U));
-    hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW, false>), dim3((unsigned)nblocks), dim3(64 * WY), 0,
+    hipLaunchKernelGGL((stencil_tbl<Real, R, WY, K, Q, NTS, SW>), dim3((unsigned)nblocks), dim3(64 * WY), 0,
                        s, static_cast<const Real*>(p.in), static_cast<Real*>(p.out), ga, (Real)p.D[0], (Real)p.D[1],
                        (Real)p.D[2], r, done);
     HIPK_CHECK(hipGetLastError());

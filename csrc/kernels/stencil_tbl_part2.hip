@@ -11,8 +11,8 @@ namespace hip {
 #define H3D_SEL3(...)
 #undef H3D_SEL2
 #define H3D_SEL2(...) __VA_ARGS__
-#define H3D_V(T, R, WY, K, Q, N, S, W, P) \
-  H3D_SEL##P(template void launch_tbl<T, R, WY, K, Q, N, S, W>(const StencilParams&, const KernelSpec&, hipStream_t);)
+#define H3D_V(T, R, WY, K, Q, N, S, P) \
+  H3D_SEL##P(template void launch_tbl<T, R, WY, K, Q, N, S>(const StencilParams&, const KernelSpec&, hipStream_t);)
 #include "stencil_tbl_variants.inc"
 #undef H3D_V
 

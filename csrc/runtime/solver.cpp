@@ -342,30 +342,9 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     local_.push_back(l);
   }
   setup_faces();
-  // chunked halo pipeline: overlapped sweeps whose every face is an x face
-  // sent in place or copied locally (x-slab decompositions), bands of at
-  // least K+2 rows so that a band's boundary cone reaches one band further
-  {
-    // (the lagged check: the slabs are issued before the previous sweep's
-    // check, which they need not wait for only when it is two sweeps back)
-    bool ok = tb_overlap_ && lag_ && !ordered_halo_ && cfg_.halo_chunks != 1;
-    int64_t ny = INT64_MAX;
-    for (const auto& l : local_) {
-      ny = std::min(ny, l.sd.n[1]);
-      for (const auto& io : l.faces) ok &= face_axis(io.face) == 0 && (io.contiguous || io.peer_local >= 0);
-    }
-    int M = cfg_.halo_chunks > 1 ? cfg_.halo_chunks : 1;
-    while (M > 1 && ny / M < K_ + 3) --M;
-    if (ok && M > 1) {
-      // every local subdomain of an x-slab decomposition has the same ny
-      for (const auto& l : local_) ok &= l.sd.n[1] == ny;
-      hch_ = ok ? M : 1;
-      for (int c = 0; c <= hch_ && hch_ > 1; ++c) ych_.push_back(ny * c / hch_);
-    }
-  }
   // boundary pieces on the compute stream, after the interior: explicit only
   // for now (auto = the comm stream)
-  bcomp_ = tb_overlap_ && hch_ <= 1 && cfg_.boundary_stream == 1;
+  bcomp_ = tb_overlap_ && cfg_.boundary_stream == 1;
   dstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
   hstate_ = static_cast<DeviceState*>(be_->alloc_host(2 * sizeof(DeviceState)));
   std::memset(hstate_, 0, 2 * sizeof(DeviceState));
@@ -840,15 +819,7 @@ void Solver::enqueue_halo(int p, StreamId s, int dv) {
 }
 
 template <typename Pred>
-void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase, int64_t ylo, int64_t yhi) {
-  const bool band = ylo != INT64_MIN || yhi != INT64_MAX;
-  auto rows = [&](Box b) {  // a face box restricted to the band (x faces span the owned rows)
-    if (band) {
-      b.lo[1] = std::max(b.lo[1], ylo);
-      b.hi[1] = std::min(b.hi[1], yhi);
-    }
-    return b;
-  };
+void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase) {
   if (comm_->all_local()) {
     for (auto& l : local_)
       for (auto& io : l.faces) {
@@ -858,7 +829,7 @@ void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase, int64_
         for (auto& nio : nb.faces)
           if (nio.face == opposite(io.face)) src = &nio.g[dv].send_box;
         HEAT3D_CHECK(src, "opposite face missing");
-        be_->copy_box(dt_, nb.field[p], nb.L, rows(*src), l.field[p], l.L, rows(io.g[dv].recv_box), s);
+        be_->copy_box(dt_, nb.field[p], nb.L, *src, l.field[p], l.L, io.g[dv].recv_box, s);
       }
   } else {
     std::vector<Transfer> xs;
@@ -867,28 +838,6 @@ void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase, int64_
       for (auto& io : l.faces) {
         if (!in_phase(io)) continue;
         const FaceGeom& fg = io.g[dv];
-        if (band) {
-          // x planes in place, one transfer per plane: layout rows [r0, r1)
-          // (the ghost rows ride with the first / last band)
-          HEAT3D_CHECK(io.contiguous && face_axis(io.face) == 0, "halo bands need in-place x faces");
-          const int64_t r0 = ylo <= 0 ? -l.L.gy : ylo, r1 = yhi >= l.sd.n[1] ? l.sd.n[1] + l.L.gy : yhi;
-          const int64_t bytes = (r1 - r0) * l.L.sy * (int64_t)esize_;
-          const int64_t np = fg.send_box.hi[0] - fg.send_box.lo[0];
-          for (int64_t i = 0; i < np; ++i) {
-            Transfer snd, rcv;
-            snd.src_rank = l.sd.rank;
-            snd.dst_rank = io.peer;
-            snd.src = base + (l.L.plane_offset(fg.send_box.lo[0] + i) + (r0 + l.L.gy) * l.L.sy) * esize_;
-            snd.bytes = bytes;
-            rcv.src_rank = io.peer;
-            rcv.dst_rank = l.sd.rank;
-            rcv.dst = base + (l.L.plane_offset(fg.recv_box.lo[0] + i) + (r0 + l.L.gy) * l.L.sy) * esize_;
-            rcv.bytes = bytes;
-            xs.push_back(snd);
-            xs.push_back(rcv);
-          }
-          continue;
-        }
         if (!io.contiguous) be_->pack_box(dt_, l.field[p], l.L, fg.send_box, io.sendbuf, s);
         Transfer snd, rcv;
         snd.src_rank = l.sd.rank;
@@ -1091,7 +1040,6 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   // previous sweep's boundary slabs (comm-stream order) — unless they were
   // thinner than d, when the previous interior wrote the rest: wait for it
   // (a long sweep right after a K-thick one, e.g. across step() calls)
-  const int prev_bnd = last_bnd_;
   if (last_bnd_ > 0 && (dv ? K_ + 1 : K_) > last_bnd_) ev_wait(kComm, EV_INT + (q ^ 1));
   last_bnd_ = lb ? K_ + 1 : K_;
   const StreamId sb = bnd_stream();
@@ -1104,118 +1052,39 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
     t.V = t.R = t.WZ = t.WY = t.NT = t.L = t.ZS = 0;
     return t;
   };
-  if (hch_ <= 1) {
-    // (boundary pieces on the compute stream: the halo sends what the
-    // previous ones wrote there; EV_HCH + 0 marks the halo landed)
-    if (bcomp_) ev_wait(kComm, EV_BND + (q ^ 1));
-    enqueue_halo(bi, kComm, dv);
-    if (bcomp_) ev_record(EV_HCH, kComm);
-  } else {
-    // [B1+B2] chunked: band c of the halo, then (boundary stream) the boundary
-    // slabs of band c-1, whose Kp-step cone reaches Kp rows into band c.
-    // Band c of the halo sends rows the previous sweep's boundary slabs of
-    // band c wrote (EV_BCH + c).  The slabs overwrite planes of nxt(bi): the
-    // previous interior read them (2 buffers) and the previous halo sent them
-    // (done: it precedes band c+1 on the comm stream).
-    ev_wait(sb, EV_INT + (q ^ 1));
-    ev_wait(sb, EV_CHK + chk_prev);
-    auto slabs = [&](int c) {
-      ev_wait(sb, EV_HCH + std::min(c + 1, hch_ - 1));
-      if (c == 0) prof_record(prof_idx_, PE_BND0, sb);
-      for (auto& l : local_)
-        for (Box b : boundary_boxes(l)) {
-          b.lo[1] = std::max(b.lo[1], ych_[c]);
-          b.hi[1] = std::min(b.hi[1], ych_[c + 1]);
-          if (!b.empty()) be_->sweep(dt_, params(l, b), bspec(b), sb);
-        }
-      ev_record(EV_BCH + c, sb);
-    };
-    be_->range_push("halo");
-    prof_record(prof_idx_, PE_HALO0, kComm);
-    for (int c = 0; c < hch_; ++c) {
-      ev_wait(kComm, EV_BCH + c);
-      enqueue_halo_phase(bi, kComm, dv, [](const FaceIO&) { return true; }, ych_[c], ych_[c + 1]);
-      ev_record(EV_HCH + c, kComm);
-      if (c > 0) slabs(c - 1);
-    }
-    prof_record(prof_idx_, PE_HALO1, kComm);
-    be_->range_pop();
-    slabs(hch_ - 1);
-    prof_record(prof_idx_, PE_BND1, sb);
-    ev_record(EV_BND + q, sb);
-  }
+  // (boundary pieces on the compute stream: the halo sends what the previous
+  // ones wrote there; EV_HALO marks the halo landed)
+  if (bcomp_) ev_wait(kComm, EV_BND + (q ^ 1));
+  enqueue_halo(bi, kComm, dv);
+  if (bcomp_) ev_record(EV_HALO, kComm);
   flush_pending_reduce();
-  // [A] interior planes, as a core and a rim.  The core's Kp-step cone
-  // reads only planes the previous sweep's interior wrote (>= prev_bnd from
-  // every face with a neighbour), so it starts as soon as that interior is
-  // done; the rim (Kp planes inside the interior's faces) also reads the
-  // previous boundary slabs and waits for them.  Without the split the whole
-  // interior waited for the previous sweep's halo + boundary chain (8-GPU
-  // slab share: ~90 us idle per sweep, profiles/rank_proxy_r04.md).  Writes
-  // stay disjoint from what the previous boundary slabs still read: they
-  // reach at most prev_bnd + Kp - 1 planes in.
+  // [A] interior planes: they read the planes the previous sweep's boundary
+  // slabs wrote.  (Round 4's core/rim split, a core that did not wait for
+  // them plus thin rims that did, lost: each 3-plane rim took 46-77 us in
+  // the thin-slab kernel, profiles/rank_proxy_r04.md.)
   ev_wait(kCompute, EV_CHK + chk_prev);
   be_->range_push("interior");
   prof_record(prof_idx_, PE_INT0, kCompute);
-  bool split = prev_bnd > 0 && cfg_.core_rim && !bcomp_;
-  std::vector<std::pair<Box, std::vector<Box>>> parts;  // per local: core, rim pieces
-  for (auto& l : local_) {
-    const Box& ib = lb ? l.tb_interior_long : l.tb_interior;
-    Box core = ib;
-    for (int a = 0; a < 3; ++a) {
-      if (hd_[a] <= 1) continue;
-      if (l.sd.has_neighbor(static_cast<Face>(2 * a))) core.lo[a] = std::max(core.lo[a], (int64_t)(prev_bnd + Kp));
-      if (l.sd.has_neighbor(static_cast<Face>(2 * a + 1)))
-        core.hi[a] = std::min(core.hi[a], l.sd.n[a] - (prev_bnd + Kp));
-    }
-    std::vector<Box> rim;
-    Box rem = ib;
-    for (int a = 0; a < 3 && !core.empty(); ++a) {
-      if (core.lo[a] > rem.lo[a]) {
-        Box p = rem;
-        p.hi[a] = core.lo[a];
-        rim.push_back(p);
-        rem.lo[a] = core.lo[a];
-      }
-      if (core.hi[a] < rem.hi[a]) {
-        Box p = rem;
-        p.lo[a] = core.hi[a];
-        rim.push_back(p);
-        rem.hi[a] = core.hi[a];
-      }
-    }
-    split &= !core.empty();
-    parts.push_back({core, rim});
-  }
-  if (split) {
-    for (std::size_t i = 0; i < local_.size(); ++i) be_->sweep(dt_, params(local_[i], parts[i].first), ks, kCompute);
-    ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of the rim's input
-    for (std::size_t i = 0; i < local_.size(); ++i)
-      for (const Box& b : parts[i].second) be_->sweep(dt_, params(local_[i], b), ks, kCompute);
-  } else {
-    ev_wait(kCompute, EV_BND + (q ^ 1));  // previous boundary slabs are part of our input
-    for (auto& l : local_) be_->sweep(dt_, params(l, lb ? l.tb_interior_long : l.tb_interior), ks, kCompute);
-  }
+  ev_wait(kCompute, EV_BND + (q ^ 1));
+  for (auto& l : local_) be_->sweep(dt_, params(l, lb ? l.tb_interior_long : l.tb_interior), ks, kCompute);
   prof_record(prof_idx_, PE_INT1, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
-  if (hch_ <= 1) {
-    // [B2] the boundary slabs, behind the halo on the comm stream (or behind
-    // the interior and the halo on the compute stream)
-    if (bcomp_) {
-      ev_wait(kCompute, EV_HCH);
-    } else {
-      ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
-      ev_wait(kComm, EV_CHK + chk_prev);
-    }
-    be_->range_push("boundary");
-    prof_record(prof_idx_, PE_BND0, sb);
-    for (auto& l : local_)
-      for (const Box& b : boundary_boxes(l)) be_->sweep(dt_, params(l, b), bspec(b), sb);
-    prof_record(prof_idx_, PE_BND1, sb);
-    be_->range_pop();
-    ev_record(EV_BND + q, sb);
+  // [B2] the boundary slabs, behind the halo on the comm stream (or behind
+  // the interior and the halo on the compute stream)
+  if (bcomp_) {
+    ev_wait(kCompute, EV_HALO);
+  } else {
+    ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
+    ev_wait(kComm, EV_CHK + chk_prev);
   }
+  be_->range_push("boundary");
+  prof_record(prof_idx_, PE_BND0, sb);
+  for (auto& l : local_)
+    for (const Box& b : boundary_boxes(l)) be_->sweep(dt_, params(l, b), bspec(b), sb);
+  prof_record(prof_idx_, PE_BND1, sb);
+  be_->range_pop();
+  ev_record(EV_BND + q, sb);
   // [C] all residuals, all checks: now, or (ordered collectives) after the
   // next sweep's halo.  With the lag nothing waits for CHK(q) before sweep
   // q+2; without it sweep q+1's interior does, and is issued after the flush.

@@ -130,7 +130,6 @@ class Solver {
   // long sweeps cross the halos) and whether they do
   std::array<int64_t, 3> ghost_depth() const { return {hd_[0], hd_[1], hd_[2]}; }
   bool long_halo_sweeps() const { return long_halo_; }
-  int halo_chunks() const { return hch_; }
   int boundary_on_compute() const { return bcomp_ ? 1 : 0; }
   // the overlapped sweeps' interior and boundary pieces of local subdomain i
   // (lo0, hi0, lo1, hi1, lo2, hi2 each)
@@ -233,11 +232,8 @@ class Solver {
   void enqueue_multi(int bi, int Kp = 0, bool thick = false);
   // dv: halo depth variant (FaceGeom), 1 = the K+1 planes of a long sweep
   void enqueue_halo(int bi, StreamId s, int dv = 0);
-  // rows [ylo, yhi) of the owned y range only (chunked halo; x faces): the
-  // first / last chunk also carry the ghost rows below / above
   template <typename Pred>
-  void enqueue_halo_phase(int bi, StreamId s, int dv, Pred in_phase, int64_t ylo = INT64_MIN,
-                          int64_t yhi = INT64_MAX);
+  void enqueue_halo_phase(int bi, StreamId s, int dv, Pred in_phase);
   void join_pipeline();      // every stream waits for every pipeline event
   // Collective ordering chain (ordered_collectives comms, > 1 rank): every
   // exchange / all-reduce waits for the previous one's completion event, so
@@ -306,17 +302,8 @@ class Solver {
   std::vector<std::pair<std::string, double>> sweep_costs_;  // start-up timings (ms per sweep)
   void calibrate_remainders();
   int last_bnd_ = 0;          // boundary-layer depth of the last overlapped sweep (0: none pending)
-  // Chunked halo pipeline of overlapped x-slab sweeps (--halo-chunks): the
-  // exchange runs as hch_ transfers of owned-row bands [ych_[c], ych_[c+1])
-  // on the comm stream, and the boundary slabs of band c run on the reduce
-  // stream once band c+1 has landed, so the chain halo -> boundary slabs ->
-  // next halo is no longer serial.  With the collective chain the deferred
-  // all-reduce + check go to the comm stream right behind the halo (on the
-  // reduce stream they would queue behind the boundary slabs).  1 = off.
-  int hch_ = 1;
-  std::vector<int64_t> ych_;
-  StreamId red_stream() const { return hch_ > 1 && chain_ ? kComm : kReduce; }
-  StreamId bnd_stream() const { return hch_ > 1 ? kReduce : bcomp_ ? kCompute : kComm; }
+  StreamId red_stream() const { return kReduce; }
+  StreamId bnd_stream() const { return bcomp_ ? kCompute : kComm; }
   // boundary pieces after the interior on the compute stream (--boundary-stream)
   bool bcomp_ = false;
   bool ordered_halo_ = false; // axis-ordered exchange filling edges / corners (deep y / z halos)
@@ -349,11 +336,10 @@ class Solver {
   std::vector<Segment> segs_;       // ring of recent segments (for convergence rollback)
   std::size_t seg_head_ = 0;
 
-  // events: 0..1 int[p], 2..3 bnd[p], 4..5 check[p], 6 fork, 7 join comm, 8 join red, 9..10 poll
-  // EV_HCH + c: halo band c landed (comm stream); EV_BCH + c: boundary slabs
-  // of band c written (boundary stream), both of the latest sweep
+  // events: 0..1 int[p], 2..3 bnd[p], 4..5 check[p], 6 fork, 7 join comm, 8 join red, 9..10 poll,
+  // EV_HALO: the latest sweep's halo landed (comm stream; --boundary-stream compute)
   enum { EV_INT = 0, EV_BND = 2, EV_CHK = 4, EV_FORK = 6, EV_JCOMM = 7, EV_JRED = 8, EV_POLL = 9,
-         EV_T0 = 11, EV_T1 = 12, EV_TOKEN = 13, EV_HCH = 16, EV_BCH = 24, EV_COUNT = 32 };
+         EV_T0 = 11, EV_T1 = 12, EV_TOKEN = 13, EV_HALO = 14, EV_COUNT = 16 };
   bool chain_ = false;              // collective ordering chain active
   struct PendingReduce {
     bool valid = false;

@@ -32,8 +32,6 @@ def native_socket_worker(rank, world, port, outdir, n, eps, decomp, dtype, extra
     assert s.native.comm_name == "socket"
     if "--temporal" in extra_args:
         assert s.native.temporal_blocking == (int(extra_args[list(extra_args).index("--temporal") + 1]) >= 2)
-    if "--halo-chunks" in extra_args:
-        assert s.native.halo_chunks == int(extra_args[list(extra_args).index("--halo-chunks") + 1])
     r = s.run()
     assert s.native.verify_halos() == 0  # checksums exchanged over the socket transport
     g = s.gather()
@@ -131,8 +129,6 @@ def native_rccl_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, ext
                               dtype=dtype, device=0, extra_args=list(extra_args))
     assert s.native.comm_name.startswith("rccl"), s.native.comm_name
     assert s.native.comm_transport_ranks == world
-    if "--halo-chunks" in extra_args:
-        assert s.native.halo_chunks == int(extra_args[list(extra_args).index("--halo-chunks") + 1])
     r = s.run()
     assert s.native.verify_halos() == 0  # checksums exchanged over RCCL
     g = s.gather()  # ncclSend / ncclRecv of every rank's block to rank 0

@@ -42,8 +42,7 @@ def test_rccl_self_exchange(ext, gpu):
     (2, (2, 1, 1), None),
     (2, (2, 1, 1), ["--rccl-shared"]),               # one communicator for halos and all-reduce
     (4, (2, 2, 1), None),                             # block: deep y halos, axis-ordered phases
-    (2, (2, 1, 1), ["--halo-chunks", "4"]),           # halo in row bands, boundary slabs per band
-    (3, (3, 1, 1), ["--halo-chunks", "3"]),
+    (3, (3, 1, 1), None),
 ])
 def test_rccl_multirank_bitwise(h3d, gpu, tmp_path, world, decomp, extra):
     n, eps = 33, 1e-4

@@ -103,10 +103,6 @@ def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
     assert np.array_equal(a.gather(), b.gather())
 
 
-# L = -2: the persistent walk (every block a contiguous range of the tile-major
-# (tile, plane) list, several tiles per block, a residual commit per tile);
-# instantiated for the default shapes only (stencil_tbl.hip H3D_TBLA)
-WALK = {2: [], 3: ["tl3:1:3:1:16:-2:3:2"], 4: ["tl4:1:3:1:12:-2:3:2"]}
 VARIANTS_K = {3: ["tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5:3", "tl3:1:3:1:16:0:6",
                   "tl3:1:2:1:16:7:6", "tl3:1:6:1:8:0:3", "tl3:1:3:1:16:0:3:2", "tl3:1:3:1:16:0:3:19", "tl3:1:3:1:16:0:3:0"],
               4: ["tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6",
@@ -135,7 +131,7 @@ def test_stencil_k_bitwise(h3d, gpu, K, dtype, n):
         T[1:-1, 1:-1, 1:-1] = u
         refs.append(r)
     want = T[1:-1, 1:-1, 1:-1]
-    for v in VARIANTS_K[K] + WALK[K] + (VARIANTS_K_F32[K] if dtype == torch.float32 else []):
+    for v in VARIANTS_K[K] + (VARIANTS_K_F32[K] if dtype == torch.float32 else []):
         out = ops.PaddedField(n, dtype=dtype, device=gpu)
         out.flat.fill_(-3.0)
         st = ops.new_state(gpu)
@@ -175,7 +171,7 @@ def _deep_random(ops, n, gx, dtype, seed):
     return f
 
 
-@pytest.mark.parametrize("kernel", ["tl2", "tl3", "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:0:6", "tl3:1:3:1:16:-2:3:2", "tl4:1:3:1:12:-2:3:2",
+@pytest.mark.parametrize("kernel", ["tl2", "tl3", "tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:0:6",
                                     "tl4:1:6:1:8:0:3", "tl3:1:6:1:8:0:3"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (5, (0, 5), "lo"), (9, (0, 9), "hi"),
@@ -346,7 +342,7 @@ def _deep3_random(ops, n, g, dtype, seed):
     return f
 
 
-@pytest.mark.parametrize("kernel", ["tl2", "tl3", "tl4", "tl3:1:3:1:16:0:4", "tl3:1:3:1:16:-2:3:2", "tl4:1:3:1:12:-2:3:2"])
+@pytest.mark.parametrize("kernel", ["tl2", "tl3", "tl4", "tl3:1:3:1:16:0:4"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("box,sides", [((0, 12, 0, 50, 0, 140), "lo"), ((0, 12, 0, 50, 0, 140), "hi"),
                                        ((0, 12, 0, 50, 0, 140), "both"), ((0, 12, 4, 46, 0, 140), "both"),
@@ -497,17 +493,15 @@ def test_preheat_keeps_rollback_input_gpu(h3d, gpu, vr, dims):
 
 
 @pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (8, 1, 1)), (8, (2, 2, 2)), (4, (1, 2, 2))])
-@pytest.mark.parametrize("dtype,core_rim", [("fp64", False), ("fp32", False), ("fp64", True), ("fp64", "bcomp")])
-def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype, core_rim):
+@pytest.mark.parametrize("dtype,bcomp", [("fp64", False), ("fp32", False), ("fp64", True)])
+def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype, bcomp):
     """The driver's window at N > 1 (warm-up 5, then 20 steps = 4 x 3 + 2 x 4):
     long K+1 sweeps across the halos, including the (K+1)-plane boundary
     slabs (y-marching K = 4 thin-slab tiles), bitwise equal to single steps;
-    also with ``--core-rim`` (interior as core + rim, rims wait for the
-    previous boundary slabs on the device)."""
+    also with the boundary pieces on the compute stream."""
     n = (82, 70, 150)
     a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims,
-                       extra_args=["--long-sweeps", "on"] + (["--boundary-stream", "compute"] if core_rim == "bcomp"
-                                                             else ["--core-rim"] if core_rim else []))
+                       extra_args=["--long-sweeps", "on"] + (["--boundary-stream", "compute"] if bcomp else []))
     b = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
     assert a.native.long_halo_sweeps
     a.initialize(), b.initialize()
@@ -518,29 +512,6 @@ def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype, core_rim):
         sa, sb = a.native.state(), b.native.state()
         assert sa["iter"] == sb["iter"] and sa["last_residual"] == sb["last_residual"]
         assert np.array_equal(a.gather(), b.gather()), (vr, dims, dtype, k)
-    assert a.native.verify_halos() == 0
-
-
-@pytest.mark.parametrize("vr,M", [(3, 4), (8, 3), (2, 2)])
-@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
-def test_chunked_halo_pipeline_gpu(h3d, gpu, vr, M, dtype):
-    """--halo-chunks M on real streams: band c of the halo on the comm stream,
-    the boundary slabs of band c on the reduce stream once band c+1 landed,
-    the interior on the compute stream; regular, partial and long sweeps,
-    bitwise equal to single steps."""
-    n = (82, 70, 150)
-    a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=(vr, 1, 1),
-                       extra_args=["--long-sweeps", "on", "--halo-chunks", str(M)])
-    b = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
-    assert a.native.halo_chunks == M
-    a.initialize(), b.initialize()
-    for k in (5, 20, 11, 4, 30):
-        a.step(k)
-        b.step(k)
-        a.synchronize(), b.synchronize()
-        sa, sb = a.native.state(), b.native.state()
-        assert sa["iter"] == sb["iter"] and sa["last_residual"] == sb["last_residual"]
-        assert np.array_equal(a.gather(), b.gather()), (vr, M, dtype, k)
     assert a.native.verify_halos() == 0
 
 

@@ -81,21 +81,6 @@ def test_native_socket_temporal_slabs(h3d, tmp_path, world):
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 3), (3, 2)])
-def test_native_socket_chunked_halo(h3d, tmp_path, world, chunks):
-    """--halo-chunks: the x-slab halo travels as row bands, one transfer per
-    plane and band over the socket transport (the non-local path RCCL takes),
-    each band's boundary slabs on the reduce stream; bitwise equal to the
-    single-process single-step solve."""
-    n, eps = 31, 1e-4
-    _spawn(native_socket_worker, world, str(tmp_path), n, eps, (world, 1, 1), "fp64",
-           ["--temporal", "3", "--halo-chunks", str(chunks)])
-    single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", extra_args=["--temporal", "1"])
-    r1 = single.run()
-    assert int(open(tmp_path / "result.txt").read().split()[0]) == r1["conv_iter"]
-    assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
-
-
 @pytest.mark.parametrize("world,decomp", [(4, (2, 2, 1)), (4, (1, 2, 2)), (8, (2, 2, 2))])
 def test_native_socket_temporal_blocks(h3d, tmp_path, world, decomp):
     """3-step temporal blocking across processes with y / z splits: the
