@@ -56,11 +56,16 @@ def parse_args(argv=None):
                     help="weak scaling: each GPU owns B^3 interior points, global grid = dims*B + 2 "
                          "(BASELINE config 5: B=2047 fp32 gives 4096^3 on 8 GPUs)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
-    ap.add_argument("--decomp", default="auto", help="auto | slab | block | AxBxC")
+    ap.add_argument("--decomp", default="auto",
+                    help="auto | slab | block | AxBxC.  auto: slabs, unless the start-up link probe (a K-deep "
+                         "face to both ring neighbours through the job's transport, slowest rank) measures "
+                         "less than the phantom-rank proxy's crossover (8 ranks: 55 GB/s), then 2D blocks")
+    ap.add_argument("--no-link-probe", action="store_true", help="--decomp auto without the link probe: slabs")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--graph-chunk", type=int, default=32)
+    ap.add_argument("--graph-chunk", type=int, default=0,
+                    help="iterations per hipGraph (0 = the solver's choice: 32, 96 for the overlapped N > 1 schedule)")
     ap.add_argument("--converge-eps", type=float, default=1e-5,
                     help="also measure time-to-converge at this EPS (0 disables).  Default: the reference's "
                          "tolerance 1e-5 (1024^3 fp64: 186188 iterations, 240 s on one MI355X, 21.5%% off the "
@@ -172,7 +177,7 @@ def run_rank(args) -> int:
 
     import heat3d_amd
     from heat3d_amd import HeatSolver
-    from heat3d_amd.parallel import best_dims_for
+    from heat3d_amd.parallel import SLAB_MIN_LINK_GBPS, best_dims_for, choose_dims
     from heat3d_amd.parallel.distributed import all_gather_objects, barrier, init_process_group, max_over_ranks
     from heat3d_amd.utils.metrics import roofline_glups
 
@@ -202,7 +207,22 @@ def run_rank(args) -> int:
     nparts = world * args.virtual_ranks
     if args.virtual_ranks > 1:
         assert world == 1, "--virtual-ranks is a single-process diagnostic"
-    if args.decomp in ("auto", "slab", "block"):
+    link = None
+    if args.decomp == "auto" and world > 1 and args.virtual_ranks == 1 and not args.no_link_probe:
+        # time one K-deep x face (the slab halo of a sweep) to both ring
+        # neighbours over the job's own transport, on a throw-away solver
+        # whose communicator is created like the real one; every rank gets
+        # the slowest rank's rate
+        esize = 8 if args.dtype == "fp64" else 4
+        depth = args.temporal if args.temporal >= 2 else 3
+        face = depth * (G + 2) * (G + 8) * esize
+        probe = HeatSolver((4 * world + 2, 8, 8), iter_max=1, eps=0.0, dtype=args.dtype, backend="hip",
+                           decomp=(world, 1, 1), device=dev, group=group, comm=args.comm,
+                           extra_args=["--watchdog", str(args.watchdog)])
+        link = probe.native.link_probe(face, 5)
+        del probe
+        dims = choose_dims(N, nparts, link)
+    elif args.decomp in ("auto", "slab", "block"):
         dims = best_dims_for(N, nparts, None if args.decomp == "auto" else args.decomp)
     else:
         dims = tuple(int(v) for v in args.decomp.lower().split("x"))
@@ -287,6 +307,8 @@ def run_rank(args) -> int:
     # remainder policy (Solver::calibrate_remainders): which n mod K end in
     # K+1-step sweeps, from the start-up sweep timings (ms)
     placement = all_gather_objects({"rank": rank, "device": dev, "host": socket.gethostname(),
+                                    "link_probe_gbps": None if link is None else round(link, 3),
+                                    "dims": list(dims), "rccl_p2p_channels": s.native.rccl_p2p_channels or None,
                                     "subdomain": list(s.native.local_subdomain(0)["n"]), "x_schedules": xs,
                                     "long_remainders": list(s.native.long_remainders),
                                     "sweep_costs_ms": {k: round(v, 4) for k, v in s.native.sweep_costs.items()}},
@@ -345,6 +367,11 @@ def run_rank(args) -> int:
                    "overlap": not args.no_overlap, "comm": comm_name, "reserved_cus": reserved,
                    "preheat_sweeps": preheat},
         "comm_ranks": comm_ranks,
+        # --decomp auto: the start-up link probe (slowest rank's one-way GB/s
+        # per link) against the proxy's slab / 2D-block crossover
+        "decomp_auto": None if link is None else {"link_probe_gbps": round(link, 3),
+                                                   "slab_min_gbps": SLAB_MIN_LINK_GBPS.get(world),
+                                                   "dims": list(dims)},
         "placement": placement,
         "halo_verified": True,
         "headline_config": is_headline,

@@ -107,7 +107,14 @@ std::string rccl_version();
 // ncclCommSplit); graph: its calls may be recorded into hipGraphs.
 struct RcclOptions {
   bool shared = false, graph = false;
+  // RCCL's P2P channel pool (NCCL_MAX_P2P_NCHANNELS, exported before the
+  // first communicator of the process unless the environment sets it):
+  // > 0 that many, 0 = leave RCCL's default
+  int p2p_channels = 0;
 };
+// The NCCL_MAX_P2P_NCHANNELS this process's communicators were created
+// with ("" = RCCL's default)
+std::string rccl_p2p_channels_env();
 std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::string& unique_id, int device,
                                      const RcclOptions& o = {});
 

@@ -48,12 +48,17 @@ class PhantomComm final : public Comm {
     // bytes / (GB/s) in us, every peer's channels in flight at once
     const double wire = worst && gbps_ > 0 ? worst / (gbps_ * 1e3) : 0.0;
     const int blocks = channels_ * (int)per_peer.size();
+    // one clock stamp per stream: exchanges queued on different streams
+    // (single-step halos, overlapped sweeps) must not share the stamp an
+    // earlier delay_since still reads
+    void* stamp = nullptr;
     if (overlap_ && wire > 0) {
       if (!slot_) {
         be_ = &be;
-        slot_ = be.alloc(8);
+        slot_ = be.alloc(8 * kNumStreams);
       }
-      be.stamp(slot_, s);
+      stamp = static_cast<char*>(slot_) + 8 * (int)s;
+      be.stamp(stamp, s);
     } else if (wire > 0) {
       be.delay(wire, s, blocks);
     }
@@ -64,7 +69,7 @@ class PhantomComm final : public Comm {
         if (y.src_rank == rank_ && y.bytes == x.bytes) src = y.src;
       if (src) be.copy(x.dst, src, x.bytes, CopyKind::D2D, s);
     }
-    if (overlap_ && wire > 0) be.delay_since(slot_, wire, s, blocks);
+    if (overlap_ && wire > 0) be.delay_since(stamp, wire, s, blocks);
   }
   void allreduce(void*, std::size_t, RedType, RedOp, Backend& be, StreamId s) override {
     if (ar_us_ > 0) be.delay(ar_us_, s, ar_channels_);
@@ -79,7 +84,7 @@ class PhantomComm final : public Comm {
   int channels_, ar_channels_;
   bool overlap_;
   Backend* be_ = nullptr;  // owner of slot_ (outlives the communicator, ~Solver)
-  void* slot_ = nullptr;   // device clock stamp of the exchange in flight
+  void* slot_ = nullptr;   // device clock stamps of the exchanges in flight, one per stream
 };
 
 }  // namespace

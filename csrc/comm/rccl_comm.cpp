@@ -89,6 +89,11 @@ class RcclComm final : public Comm {
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     if (hipSetDevice(device) != hipSuccess) HEAT3D_THROW("hipSetDevice(" << device << ") failed");
+    // P2P channel pool sized to the CUs the overlapped schedule keeps free
+    // of the interior sweep (RCCL reads it at communicator initialisation;
+    // an explicit NCCL_MAX_P2P_NCHANNELS in the environment wins)
+    if (o.p2p_channels > 0 && !std::getenv("NCCL_MAX_P2P_NCHANNELS"))
+      setenv("NCCL_MAX_P2P_NCHANNELS", std::to_string(o.p2p_channels).c_str(), 0);
     NCCL_CHECK(ncclCommInitRank(&halo_, size_, id, rank_));
     int n = 0;
     NCCL_CHECK(ncclCommCount(halo_, &n));
@@ -109,7 +114,7 @@ class RcclComm final : public Comm {
   int size() const override { return size_; }
   std::vector<int> local_ranks() const override { return {rank_}; }
   bool device_buffers() const override { return true; }
-  // RCCL calls are recorded into hipGraphs only with --rccl-graph
+  // RCCL calls are recorded into hipGraphs unless --no-rccl-graph (Config::rccl_graph, default on)
   bool capturable() const override { return graph_; }
   int transport_ranks() const override {
     int n = 0;
@@ -182,6 +187,11 @@ class RcclComm final : public Comm {
 };
 
 }  // namespace
+
+std::string rccl_p2p_channels_env() {
+  const char* e = std::getenv("NCCL_MAX_P2P_NCHANNELS");
+  return e ? std::string(e) : std::string();
+}
 
 std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::string& unique_id, int device,
                                      const RcclOptions& o) {

@@ -123,9 +123,12 @@ std::string Config::usage() {
      << "                            GPU only, measure = on any backend)\n"
      << "  --autotune auto|on|off    time the sweep schedule candidates (z stride, x segments) at start-up;\n"
      << "                            auto: single-subdomain runs (--no-autotune = off)\n"
-     << "  --graph-multistream       record the overlapped multi-stream schedule into hipGraphs too\n"
+     << "  --no-stream-graphs        run the overlapped multi-stream schedule eagerly (default: one linear\n"
+     << "                            hipGraph per stream, device-side cross-stream waits)\n"
      << "  --no-rccl-graph           never record RCCL calls into hipGraphs (eager multi-rank steps)\n"
      << "  --rccl-shared             one RCCL communicator for halos and all-reduces\n"
+     << "  --rccl-p2p-channels N     RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS unless set in the\n"
+     << "                            environment): 0 auto = the reserved CUs (8), -1 RCCL's default\n"
      << "  --mem-reserve-gb G        memory preflight reserve (default 2)\n"
      << "  --no-mem-preflight        skip the memory preflight\n"
      << "  --host-mem-limit-gb G     host RAM budget of the gather-to-root Tecplot (default RAM/2)\n"
@@ -268,10 +271,12 @@ Config Config::parse(int argc, const char* const* argv) {
       else if (v == "off") c.autotune = 0;
       else throw UsageError("--autotune auto|on|off, not '" + v + "'");
     }
-    else if (key == "--graph-multistream") c.graph_multistream = true;
+    else if (key == "--no-stream-graphs") c.stream_graphs = false;
+    else if (key == "--stream-graphs") c.stream_graphs = true;
     else if (key == "--rccl-graph") c.rccl_graph = true;
     else if (key == "--no-rccl-graph") c.rccl_graph = false;
     else if (key == "--rccl-shared") c.rccl_shared = true;
+    else if (key == "--rccl-p2p-channels") c.rccl_p2p_channels = (int)to_i64(get("--rccl-p2p-channels"), "--rccl-p2p-channels");
     else if (key == "--mem-reserve-gb") c.mem_reserve_gb = to_f64(get("--mem-reserve-gb"), "--mem-reserve-gb");
     else if (key == "--no-mem-preflight") c.mem_preflight = false;
     else if (key == "--host-mem-limit-gb") c.host_mem_limit_gb = to_f64(get("--host-mem-limit-gb"), "--host-mem-limit-gb");
@@ -308,7 +313,8 @@ Config Config::parse(int argc, const char* const* argv) {
   if (c.gpus < 0) throw UsageError("--gpus must be >= 1");
   if (c.gpus > 1 && c.virtual_ranks > 1) throw UsageError("--gpus and --virtual-ranks are exclusive");
   if (c.check_every < 1) c.check_every = 1;
-  if (c.graph_chunk < 2) c.graph_chunk = 2;
+  if (c.graph_chunk < 0) c.graph_chunk = 0;
+  if (c.graph_chunk == 1) c.graph_chunk = 2;
   if (c.graph_chunk % 2) c.graph_chunk += 1;
   if (c.io_stage_mb < 1) c.io_stage_mb = 1;
   if (c.watchdog_s <= 0) throw UsageError("--watchdog must be > 0");

@@ -49,7 +49,8 @@ struct Config {
   bool use_graph = true;
   bool overlap = true;
   int check_every = 64;                   // host poll period for the device convergence flag
-  int graph_chunk = 32;                   // iterations per captured hipGraph (rounded to even)
+  int graph_chunk = 0;                    // iterations per captured hipGraph (rounded to even; 0 = auto:
+                                          // 32, 96 for the overlapped multi-stream schedule)
   std::string kernel = "auto";            // stencil kernel variant
   std::string kernel2 = "auto";           // 2-step temporally blocked kernel variant
   int temporal = 0;                       // 0 auto (2 on GPU without halos), 1 off, 2 on
@@ -90,9 +91,11 @@ struct Config {
   // time the interior sweeps' schedule candidates at initialisation: -1 auto
   // (single-subdomain runs, whose sweeps run alone as they are timed), 0 off, 1 on
   int autotune = -1;
-  bool graph_multistream = false; // record the overlapped multi-stream schedule into hipGraphs too
+  bool stream_graphs = true;      // overlapped multi-stream schedules as hipGraphs too (one linear graph
+                                  // per stream; --no-stream-graphs: eager)
   bool rccl_graph = true;         // RCCL calls may be recorded into hipGraphs (tests/test_gpu_rccl.py)
   bool rccl_shared = false;       // one RCCL communicator for halos and all-reduces (else ncclCommSplit)
+  int rccl_p2p_channels = 0;      // RCCL P2P channel pool: 0 auto (the reserved CUs, 8), -1 RCCL's default
   double mem_reserve_gb = 2.0;    // memory preflight: reserve for RCCL, code objects, scratch
   bool mem_preflight = true;      // refuse configurations that do not fit before allocating
   double host_mem_limit_gb = 0;   // gather-to-root Tecplot: host RAM budget (0 = half of RAM)

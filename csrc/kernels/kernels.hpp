@@ -137,6 +137,14 @@ void stamp(void* slot, void* stream);
 void delay_since(const void* slot, double us, void* stream, int blocks = 1);
 // placement probe: out[b] = XCC << 8 | SE/SH/CU id of workgroup b (blocks x 64 threads)
 void cu_probe(unsigned* out, int blocks, double us, void* stream);
+// Device-side stream dependencies of per-stream hipGraphs (hip_backend.cpp):
+// signal stores 1 into *slot (release, agent scope) once the work before it on
+// its stream is complete; wait spins (acquire) until its slots are != 0.  A wait that
+// outlasts `timeout_s` sets st->fault = 2 and st->done (every later sweep is
+// then a no-op) and returns, so a broken dependency cannot hang the GPU.
+void graph_signal(unsigned* slot, void* stream);
+// (wait: on every one of `n` <= 4 slots)
+void graph_wait(const unsigned* const* slots, int n, DeviceState* st, double timeout_s, void* stream);
 // Adds Σ|T - y| and the point count over `box` into s->error_sum/error_count.
 // `scratch` must hold at least error_scratch_elems() doubles.
 void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,

@@ -771,6 +771,43 @@ void cu_probe(unsigned* out, int blocks, double us, void* stream) {
   HIPK_CHECK(hipGetLastError());
 }
 
+__global__ void graph_signal_kernel(unsigned* slot) {
+  if (threadIdx.x == 0) __hip_atomic_store(slot, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct WaitSlots {
+  const unsigned* p[4];
+};
+
+__global__ void graph_wait_kernel(WaitSlots w, int n, DeviceState* st, unsigned long long ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < n; ++i) {
+    while (__hip_atomic_load(w.p[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+        __hip_atomic_store(&st->fault, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st->done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+}
+
+void graph_signal(unsigned* slot, void* stream) {
+  hipLaunchKernelGGL(graph_signal_kernel, dim3(1), dim3(64), 0, S(stream), slot);
+  HIPK_CHECK(hipGetLastError());
+}
+
+void graph_wait(const unsigned* const* slots, int n, DeviceState* st, double timeout_s, void* stream) {
+  HEAT3D_CHECK(n >= 1 && n <= 4 && st, "graph_wait: 1..4 slots and a state");
+  WaitSlots w{};
+  for (int i = 0; i < n; ++i) w.p[i] = slots[i];
+  hipLaunchKernelGGL(graph_wait_kernel, dim3(1), dim3(64), 0, S(stream), w, n, st,
+                     (unsigned long long)(timeout_s * 1e8));  // 100 MHz real-time clock
+  HIPK_CHECK(hipGetLastError());
+}
+
 __global__ void delay_kernel(unsigned long long ticks) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);

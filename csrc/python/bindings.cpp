@@ -679,6 +679,10 @@ PYBIND11_MODULE(_heat3d, m) {
         py::gil_scoped_release nogil;
         return s.verify_halos();
       })
+      .def("link_probe", [](Solver& s, std::size_t bytes, int reps) {
+        py::gil_scoped_release nogil;
+        return s.link_probe(bytes, reps);
+      }, py::arg("bytes"), py::arg("reps") = 5)
       .def("set_phase_timing", &Solver::set_phase_timing)
       .def("phase_times", &Solver::phase_times)
       .def("profile_sweeps", [](Solver& s, int n) {
@@ -732,6 +736,7 @@ PYBIND11_MODULE(_heat3d, m) {
                              })
       .def_property_readonly("backend_name", [](Solver& s) { return std::string(s.backend().name()); })
       .def_property_readonly("comm_name", [](Solver& s) { return std::string(s.comm().name()); })
+      .def_property_readonly("rccl_p2p_channels", [](Solver&) { return rccl_p2p_channels_env(); })
       .def_property_readonly("comm_size", [](Solver& s) { return s.comm().size(); })
       .def_property_readonly("dims", [](Solver& s) { return s.decomposition().topo.dims; })
       .def_property_readonly("physics", [](Solver& s) {

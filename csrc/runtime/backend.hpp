@@ -64,13 +64,23 @@ class Backend {
   virtual void sync(StreamId s) = 0;
   virtual void sync_all() = 0;
 
-  // Graph recording: between begin_capture and end_capture nothing runs;
-  // every operation on any stream becomes a node of one graph, and event
-  // record / wait pairs become its dependency edges (HipBackend builds the
-  // graph explicitly, see hip_backend.cpp).  The executable graph is launched
-  // on the compute stream.
+  // Graph recording: between begin_capture and end_capture nothing runs.
+  //   * one graph (per_stream = false): every operation on any stream becomes
+  //     a node of one graph, and event record / wait pairs become its
+  //     dependency edges (HipBackend builds the graph explicitly, see
+  //     hip_backend.cpp).  The executable graph is launched on the compute
+  //     stream (a DAG with parallel branches: the HIP runtime replays them
+  //     on streams of its own, without the CU mask and priorities).
+  //   * one linear graph per stream (per_stream = true): each stream's
+  //     operations in issue order, launched on that stream (CU mask and
+  //     priority kept); a wait on an event another stream recorded inside
+  //     the recording becomes a device-side wait on a signal slot, set by
+  //     the recording stream (kernels graph_signal / graph_wait).  A wait
+  //     that times out marks `fault_state` (fault = 2, done = 1).
+  // launch_graph joins every stream into the compute stream afterwards.
   virtual bool supports_graphs() const { return false; }
-  virtual void begin_capture() {}
+  virtual void begin_capture(bool /*per_stream*/ = false, DeviceState* /*fault_state*/ = nullptr,
+                             int /*max_signals*/ = 0) {}
   virtual void* end_capture() { return nullptr; }  // returns executable graph
   virtual void launch_graph(void* /*exec*/) {}
   virtual void destroy_graph(void* /*exec*/) {}

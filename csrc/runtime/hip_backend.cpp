@@ -16,6 +16,19 @@
 // child-graph node, or one-kernel captures re-added as kernel nodes — replayed
 // without overlap or broke ordering on HIP 7.2 and were removed.)
 //
+// That DAG suits single-stream schedules.  A DAG with parallel branches is
+// replayed by the HIP runtime on streams of its own, without the compute
+// stream's CU mask and the comm stream's priority: the overlapped multi-rank
+// schedule ran 1.7x slower as one (profiles/rank_proxy_r04.md).  So those
+// schedules record one LINEAR graph per stream, each launched on its own
+// stream — a linear graph launched on the CU-masked stream stays on its 248
+// CUs (tools/probes/graph_streams_probe.hip) — and their cross-stream
+// dependencies become device-side signal / wait kernels on slots reset
+// before every launch.  (Captured hipStreamWaitValue64 nodes did not hold
+// their wait on HIP 7.2: the same probe.)  An event wait resolves on the
+// device when the work runs, not when it is enqueued, so each stream's graph
+// can be launched whole although the streams depend on each other within it.
+//
 // The device is bound once (the reference called cudaSetDevice(rank % n) in
 // every iteration, heat3D.cu:650-654).  The comm and reduce streams get the
 // highest priority so that halo pack / boundary / convergence kernels are
@@ -99,6 +112,12 @@ class HipBackend final : public Backend {
   ~HipBackend() override {
     (void)hipSetDevice(dev_);
     if (rec_) (void)hipGraphDestroy(rec_);
+    for (auto& g : recs_)
+      if (g) (void)hipGraphDestroy(g);
+    if (sig_) (void)hipFree(sig_);
+    if (fork_ev_) (void)hipEventDestroy(fork_ev_);
+    for (auto& e : join_ev_)
+      if (e) (void)hipEventDestroy(e);
     for (auto& s : caps_)
       if (s) (void)hipStreamDestroy(s);
     if (err_scratch_) (void)hipFree(err_scratch_);
@@ -170,13 +189,19 @@ class HipBackend final : public Backend {
   int reserved_cus() const override { return reserved_; }
   void* op_begin(StreamId s) override {
     if (!recording_) return streams_[s];
+    if (split_) flush_sync(s);
+    return cap_begin(s);
+  }
+  // open a capture of one operation on stream s straight into the graph
+  // being recorded (s's own graph in per-stream mode), behind s's frontier
+  void* cap_begin(StreamId s) {
     HEAT3D_CHECK(!in_op_, "graph recording: nested operation");
     in_op_ = true;
     op_s_ = s;
     // capture straight into the recorded graph, behind the stream's frontier
     auto& t = tail_[s];
-    HIP_CHECK(hipStreamBeginCaptureToGraph(capture_stream(s), rec_, t.empty() ? nullptr : t.data(), nullptr, t.size(),
-                                           hipStreamCaptureModeThreadLocal));
+    HIP_CHECK(hipStreamBeginCaptureToGraph(capture_stream(s), split_ ? recs_[s] : rec_, t.empty() ? nullptr : t.data(),
+                                           nullptr, t.size(), hipStreamCaptureModeThreadLocal));
     return caps_[s];
   }
   void op_end(StreamId s) override {
@@ -202,6 +227,22 @@ class HipBackend final : public Backend {
   }
   void event_destroy(Event e) override { (void)hipEventDestroy(static_cast<hipEvent_t>(e)); }
   void record(Event e, StreamId s) override {
+    if (recording_ && split_) {
+      // a signal behind everything issued on s so far: records with no
+      // operation between them share one slot (one signal kernel)
+      auto& q = pend_[s];
+      int slot;
+      if (!q.empty() && q.back().signal) {
+        slot = q.back().slots[0];
+      } else {
+        HEAT3D_CHECK(sig_n_ < sig_cap_, "per-stream graph: signal slots exhausted (" << sig_cap_ << ")");
+        slot = sig_n_++;
+        q.push_back({true, {slot}});
+        ++sig_ord_[s];
+      }
+      evsig_[e] = {slot, s, sig_ord_[s]};
+      return;
+    }
     if (recording_) {
       evn_[e] = tail_[s];  // the recording stream's frontier
       return;
@@ -209,6 +250,21 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipEventRecord(static_cast<hipEvent_t>(e), streams_[s]));
   }
   void wait(StreamId s, Event e) override {
+    if (recording_ && split_) {
+      // recorded before the recording started: complete when the graphs run
+      // (launched behind a join of every stream); same stream: stream order;
+      // an earlier wait on a later signal of the same stream covers it
+      auto it = evsig_.find(e);
+      if (it == evsig_.end() || it->second.s == s) return;
+      const Sig g = it->second;
+      int& w = waited_[s][g.s];
+      if (w >= g.ord) return;
+      w = g.ord;
+      auto& q = pend_[s];
+      if (!q.empty() && !q.back().signal && q.back().slots.size() < 4) q.back().slots.push_back(g.slot);
+      else q.push_back({false, {g.slot}});
+      return;
+    }
     if (recording_) {
       // an event recorded before the recording started is already complete
       // when the graph (launched behind a join of every stream) runs
@@ -240,9 +296,24 @@ class HipBackend final : public Backend {
   }
 
   bool supports_graphs() const override { return true; }
-  void begin_capture() override {
+  void begin_capture(bool per_stream, DeviceState* fault_state, int max_signals) override {
     HEAT3D_CHECK(!recording_, "graph recording already active");
-    HIP_CHECK(hipGraphCreate(&rec_, 0));
+    split_ = per_stream;
+    if (split_) {
+      HEAT3D_CHECK(fault_state, "per-stream graphs need a device state for wait timeouts");
+      for (auto& g : recs_) HIP_CHECK(hipGraphCreate(&g, 0));
+      sig_cap_ = std::max(16, max_signals);
+      HIP_CHECK(hipMalloc(&sig_, sizeof(unsigned) * sig_cap_));
+      sig_n_ = 0;
+      fault_ = fault_state;
+      evsig_.clear();
+      for (auto& q : pend_) q.clear();
+      for (auto& w : waited_)
+        for (int& v : w) v = 0;
+      for (int& o : sig_ord_) o = 0;
+    } else {
+      HIP_CHECK(hipGraphCreate(&rec_, 0));
+    }
     for (auto& t : tail_) t.clear();
     evn_.clear();
     in_op_ = false;
@@ -250,26 +321,83 @@ class HipBackend final : public Backend {
   }
   void* end_capture() override {
     HEAT3D_CHECK(recording_, "no graph recording active");
-    recording_ = false;
     if (in_op_) abort_op();  // an operation threw while being captured
-    hipGraph_t g = rec_;
-    rec_ = nullptr;
+    std::unique_ptr<GraphSet> gs(new GraphSet);
+    gs->per_stream = split_;
+    hipError_t err = hipSuccess;
+    if (split_) {
+      // the signals / waits still pending at the end of each stream
+      for (int s = 0; s < kNumStreams; ++s) {
+        try {
+          flush_sync(static_cast<StreamId>(s));
+        } catch (...) {
+          if (err == hipSuccess) err = hipErrorUnknown;
+        }
+      }
+    }
+    recording_ = false;
     evn_.clear();
     drop_capture_streams();
-    hipGraphExec_t ex = nullptr;
-    hipError_t e = hipGraphInstantiateWithFlags(&ex, g, hipGraphInstantiateFlagUseNodePriority);
-    (void)hipGraphDestroy(g);
-    HIP_CHECK(e);
-    // upload now (ordered on the compute stream) so that the first launch
-    // does not pay for it
-    HIP_CHECK(hipGraphUpload(ex, streams_[kCompute]));
-    return ex;
+    if (split_) {
+      split_ = false;
+      gs->slots = sig_;
+      gs->nslots = sig_n_;
+      sig_ = nullptr;
+      for (int s = 0; s < kNumStreams; ++s) {
+        std::size_t n = 0;
+        if (err == hipSuccess) err = hipGraphGetNodes(recs_[s], nullptr, &n);
+        if (err == hipSuccess && n > 0) err = hipGraphInstantiateWithFlags(&gs->ex[s], recs_[s], 0);
+        (void)hipGraphDestroy(recs_[s]);
+        recs_[s] = nullptr;
+      }
+    } else {
+      hipGraph_t g = rec_;
+      rec_ = nullptr;
+      err = hipGraphInstantiateWithFlags(&gs->ex[0], g, hipGraphInstantiateFlagUseNodePriority);
+      (void)hipGraphDestroy(g);
+    }
+    if (err != hipSuccess) {
+      destroy_graph(gs.release());
+      HIP_CHECK(err);
+    }
+    // upload now so that the first launch does not pay for it (each on the
+    // stream it will be launched on)
+    for (int s = 0; s < kNumStreams; ++s)
+      if (gs->ex[s]) HIP_CHECK(hipGraphUpload(gs->ex[s], streams_[gs->per_stream ? s : kCompute]));
+    return gs.release();
   }
-  void launch_graph(void* ex) override {
-    HIP_CHECK(hipGraphLaunch(static_cast<hipGraphExec_t>(ex), streams_[kCompute]));
+  void launch_graph(void* h) override {
+    auto* g = static_cast<GraphSet*>(h);
+    if (!g->per_stream) {
+      HIP_CHECK(hipGraphLaunch(g->ex[0], streams_[kCompute]));
+      return;
+    }
+    // The solver launches behind a join of every stream into the compute
+    // stream: reset the signal slots there, fork, launch each stream's graph
+    // on its stream, join back into the compute stream.
+    if (!fork_ev_) {
+      HIP_CHECK(hipEventCreateWithFlags(&fork_ev_, hipEventDisableTiming));
+      for (auto& e : join_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (g->nslots) HIP_CHECK(hipMemsetAsync(g->slots, 0, sizeof(unsigned) * g->nslots, streams_[kCompute]));
+    HIP_CHECK(hipEventRecord(fork_ev_, streams_[kCompute]));
+    for (int s = kComm; s < kNumStreams; ++s)
+      if (g->ex[s]) HIP_CHECK(hipStreamWaitEvent(streams_[s], fork_ev_, 0));
+    for (int s = 0; s < kNumStreams; ++s)
+      if (g->ex[s]) HIP_CHECK(hipGraphLaunch(g->ex[s], streams_[s]));
+    for (int s = kComm; s < kNumStreams; ++s)
+      if (g->ex[s]) {
+        HIP_CHECK(hipEventRecord(join_ev_[s], streams_[s]));
+        HIP_CHECK(hipStreamWaitEvent(streams_[kCompute], join_ev_[s], 0));
+      }
   }
-  void destroy_graph(void* ex) override {
-    if (ex) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(ex));
+  void destroy_graph(void* h) override {
+    auto* g = static_cast<GraphSet*>(h);
+    if (!g) return;
+    for (auto& e : g->ex)
+      if (e) (void)hipGraphExecDestroy(e);
+    if (g->slots) (void)hipFree(g->slots);
+    delete g;
   }
 
   void init_field(DType t, const InitParams& p, StreamId s) override {
@@ -320,6 +448,50 @@ class HipBackend final : public Backend {
   }
 
  private:
+  // per-stream recording: the signal / wait kernels pending on each stream,
+  // emitted in order before its next operation (consecutive waits merged)
+  struct SyncItem {
+    bool signal;
+    std::vector<int> slots;
+  };
+  struct Sig {
+    int slot;
+    StreamId s;
+    int ord;  // the how-manieth signal of stream s
+  };
+  void flush_sync(StreamId s) {
+    auto& q = pend_[s];
+    if (q.empty()) return;
+    std::vector<SyncItem> items;
+    items.swap(q);
+    for (const SyncItem& it : items) {
+      hipStream_t st = static_cast<hipStream_t>(cap_begin(s));
+      try {
+        if (it.signal) {
+          hip::graph_signal(sig_ + it.slots[0], st);
+        } else {
+          const unsigned* p[4];
+          for (std::size_t i = 0; i < it.slots.size(); ++i) p[i] = sig_ + it.slots[i];
+          hip::graph_wait(p, (int)it.slots.size(), fault_, kGraphWaitTimeoutS, st);
+        }
+      } catch (...) {
+        abort_op();
+        throw;
+      }
+      op_end(s);
+    }
+  }
+  // a device-side wait longer than this is a broken dependency (or a peer
+  // that stopped): the kernel gives up and flags the fault instead of
+  // holding the GPU
+  static constexpr double kGraphWaitTimeoutS = 60.0;
+  struct GraphSet {
+    bool per_stream = false;
+    hipGraphExec_t ex[kNumStreams] = {nullptr, nullptr, nullptr};
+    unsigned* slots = nullptr;  // per-stream graphs: signal slots
+    int nslots = 0;
+  };
+
   // run one operation: directly on the stream, or recorded as a graph node
   template <typename F>
   void op(StreamId s, F&& f) {
@@ -355,6 +527,17 @@ class HipBackend final : public Backend {
   std::vector<hipGraphNode_t> tail_[kNumStreams];    // dependency frontier per stream
   hipStream_t caps_[kNumStreams] = {nullptr, nullptr, nullptr};
   std::unordered_map<Event, std::vector<hipGraphNode_t>> evn_;  // event -> frontier at record
+  // per-stream recording
+  bool split_ = false;
+  hipGraph_t recs_[kNumStreams] = {nullptr, nullptr, nullptr};
+  unsigned* sig_ = nullptr;
+  int sig_cap_ = 0, sig_n_ = 0;
+  DeviceState* fault_ = nullptr;
+  std::unordered_map<Event, Sig> evsig_;
+  std::vector<SyncItem> pend_[kNumStreams];
+  int waited_[kNumStreams][kNumStreams] = {};  // [waiter][signaller]: highest signal waited for
+  int sig_ord_[kNumStreams] = {};
+  hipEvent_t fork_ev_ = nullptr, join_ev_[kNumStreams] = {nullptr, nullptr, nullptr};
   double* err_scratch_ = nullptr;
   Roctx roctx_;
 };

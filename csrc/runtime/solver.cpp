@@ -758,6 +758,60 @@ void Solver::calibrate_remainders() {
   be_->sync_all();
 }
 
+double Solver::link_probe(std::size_t bytes, int reps) {
+  if (comm_->all_local() || comm_->size() < 2 || bytes == 0) return 0.0;
+  const int r = process_rank(), n = comm_->size();
+  const int up = (r + 1) % n, dn = (r + n - 1) % n;
+  const int npeer = up == dn ? 1 : 2;
+  struct Bufs {  // released on every exit
+    Backend* be;
+    void *s = nullptr, *d = nullptr;
+    ~Bufs() {
+      be->release(s);
+      be->release(d);
+    }
+  } b{be_.get(), be_->alloc(npeer * bytes), be_->alloc(npeer * bytes)};
+  be_->memset(b.s, 0, npeer * bytes, kComm);
+  std::vector<Transfer> xs;
+  const int peers[2] = {up, dn};
+  for (int i = 0; i < npeer; ++i) {
+    Transfer snd, rcv;
+    snd.src_rank = r;
+    snd.dst_rank = peers[i];
+    snd.src = static_cast<char*>(b.s) + i * bytes;
+    snd.bytes = bytes;
+    // the message from peer i arrives in slot i
+    rcv.src_rank = peers[i];
+    rcv.dst_rank = r;
+    rcv.dst = static_cast<char*>(b.d) + i * bytes;
+    rcv.bytes = bytes;
+    xs.push_back(snd);
+    xs.push_back(rcv);
+  }
+  be_->sync_all();
+  double best = 1e30;
+  for (int i = 0; i < 2 + std::max(1, reps); ++i) {
+    comm_->barrier(*be_);
+    const double t0 = now_s();
+    comm_->exchange(xs, *be_, kComm);
+    be_->sync(kComm);
+    const double t = now_s() - t0;
+    if (i >= 2) best = std::min(best, t);  // two warm-up exchanges (connection setup)
+  }
+  comm_->check_async_error();
+  // the slowest rank decides: max over ranks of 2^62 - rate (in MB/s)
+  const double mbps = (double)bytes / std::max(best, 1e-9) / 1e6;
+  const unsigned long long big = 1ull << 62;
+  unsigned long long v = big - (unsigned long long)std::max(0.0, std::min(mbps, 1e15));
+  void* d = be_->alloc(8);
+  be_->copy(d, &v, 8, CopyKind::H2D, kReduce);
+  comm_->allreduce(d, 1, RedType::U64, RedOp::Max, *be_, kReduce);
+  be_->copy(&v, d, 8, CopyKind::D2H, kReduce);
+  be_->sync(kReduce);
+  be_->release(d);
+  return (double)(big - v) / 1e3;
+}
+
 int Solver::preheat(int sweeps) {
   if (!tb_ || sweeps <= 0) return 0;
   // Ordered behind every issued sweep and convergence check (join_pipeline),
@@ -1292,7 +1346,12 @@ int Solver::graph_len_for(int64_t n) const {
   int cyc;
   if (tb_) cyc = K_ * (nbuf_ == 3 ? 6 : 2);
   else cyc = nbuf_ == 3 ? 6 : 2;
-  int G = std::max(cyc, cfg_.graph_chunk - cfg_.graph_chunk % cyc);
+  // auto: 32 iterations, 96 for the overlapped multi-stream schedule, whose
+  // per-stream graphs start and end joined (each launch drains the halo /
+  // boundary / all-reduce pipeline once: ~0.12 ms on the 8-GPU slab share,
+  // 3% of 32-iteration chunks; profiles/graph_streams_r05.md)
+  const int chunk = cfg_.graph_chunk > 0 ? cfg_.graph_chunk : multi_stream() ? 96 : 32;
+  int G = std::max(cyc, chunk - chunk % cyc);
   if (n < G) G = (int)(n - n % cyc);
   return G;
 }
@@ -1311,17 +1370,14 @@ int Solver::long_sweeps_for(int64_t n) const {
 }
 
 bool Solver::graphs_allowed() const {
-  // Multi-stream (overlapped) schedules can be graphs too (built explicitly by
-  // the backend's recorder, bitwise equal to eager runs: tests/test_gpu_graph.py),
-  // but only with --graph-multistream: the HIP runtime replays the
-  // graph's parallel branches without stream priorities, so the boundary
-  // slabs and halo copies compete with the interior sweep (phantom rank of the
-  // 8-GPU bench: 0.28 ms/step as a graph, 0.21 eager; profiles/rank_proxy_r02.md)
-  // and the overlapped schedule runs eagerly — its host cost is far below its
-  // GPU time at these sizes.
-  const bool ms_ok = cfg_.graph_multistream;
+  // Multi-stream (overlapped) schedules replay one linear graph per stream,
+  // each on its own stream with its CU mask and priority, the cross-stream
+  // dependencies as device-side signal / wait kernels (HipBackend,
+  // Backend::begin_capture).  (One fork/join DAG, the round-2..4 form, was
+  // replayed by the HIP runtime on streams of its own without either: 0.366
+  // against 0.212 ms/step eager on the 8-GPU slab share, profiles/rank_proxy_r04.md.)
   return cfg_.use_graph && be_->supports_graphs() && comm_->capturable() && !graph_failed_ && !phase_timing_ &&
-         (!multi_stream() || ms_ok);
+         (!multi_stream() || cfg_.stream_graphs);
 }
 
 Solver::GraphEntry* Solver::find_graph(int G) {
@@ -1341,10 +1397,12 @@ void Solver::destroy_graphs() {
 }
 
 // Capture G iterations, as run_chunk would issue them eagerly from the current
-// state, into one graph on the compute stream; the comm / reduce streams fork
-// from it and join back into it (fresh events for every record inside the
-// capture).  The solver's host-side schedule state is restored afterwards: a
-// launch advances it exactly like the eager path.
+// state (fresh events for every record inside the capture): single-stream
+// schedules into one graph on the compute stream, whose comm / reduce
+// branches fork from it and join back into it; multi-stream schedules into
+// one linear graph per stream (the backend forks and joins the streams around
+// their launch).  The solver's host-side schedule state is restored
+// afterwards: a launch advances it exactly like the eager path.
 Solver::GraphEntry* Solver::build_graph(int G) {
   H3D_TRACE("build_graph G=" << G << " at issued=" << issued_);
   join_pipeline();
@@ -1364,13 +1422,16 @@ Solver::GraphEntry* Solver::build_graph(int G) {
   while (cap_pool_.size() < need) cap_pool_.push_back(be_->event_create());
   cap_next_ = 0;
   arm_segv_trace();
+  const bool split = multi_stream();
   try {
-    be_->begin_capture();
+    be_->begin_capture(split, dstate_, (int)need);
     capturing_ = true;
     for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
-    ev_record(EV_FORK, kCompute);
-    ev_wait(kComm, EV_FORK);
-    ev_wait(kReduce, EV_FORK);
+    if (!split) {
+      ev_record(EV_FORK, kCompute);
+      ev_wait(kComm, EV_FORK);
+      ev_wait(kReduce, EV_FORK);
+    }
     last_kind_ = e.kind;
     if (e.kind == 2) {
       for (int i = 0; i < G / K_; ++i) {
@@ -1386,10 +1447,12 @@ Solver::GraphEntry* Solver::build_graph(int G) {
       }
     }
     flush_pending_reduce();
-    ev_record(EV_JCOMM, kComm);
-    ev_record(EV_JRED, kReduce);
-    ev_wait(kCompute, EV_JCOMM);
-    ev_wait(kCompute, EV_JRED);
+    if (!split) {
+      ev_record(EV_JCOMM, kComm);
+      ev_record(EV_JRED, kReduce);
+      ev_wait(kCompute, EV_JCOMM);
+      ev_wait(kCompute, EV_JRED);
+    }
     H3D_TRACE("end_capture");
     capturing_ = false;
     e.exec = be_->end_capture();
@@ -1530,10 +1593,16 @@ RunResult Solver::run() {
   comm_->barrier(*be_);
   be_->sync_all();
   const double t0 = now_s();
-  // poll chunks hold whole pairs of K-step sweeps, so that temporally blocked
-  // runs stay aligned with their graphs and never fall back to single steps
-  const int64_t K = tb_ ? std::max<int64_t>(2 * K_, cfg_.check_every - cfg_.check_every % (2 * K_))
-                        : std::max(1, cfg_.check_every);
+  // poll chunks hold whole schedule cycles (graph_len_for), so that
+  // temporally blocked runs stay aligned with their graphs and never fall
+  // back to single steps; with graphs at least one whole graph, whose launch
+  // joins the streams (the overlapped schedule drains its pipeline there)
+  int64_t K = std::max(1, cfg_.check_every);
+  if (tb_) {
+    const int64_t cyc = (int64_t)K_ * (nbuf_ == 3 ? 6 : 2);
+    if (graphs_allowed()) K = std::max<int64_t>(K, graph_len_for(INT32_MAX));
+    K = std::max(cyc, K - K % cyc);
+  }
   const std::size_t poll_bytes = cfg_.verbose > 0 ? sizeof(DeviceState) : offsetof(DeviceState, hist);
   int pslot = 0;
   bool have_prev = false, stop = false;
@@ -1543,8 +1612,8 @@ RunResult Solver::run() {
   int64_t printed = issued_;
   const int64_t iter0 = issued_;
   double last_beat = t0;
-  int64_t iter_cap = cfg_.iter_max;        // --time-limit lowers it once
-  bool capped = cfg_.time_limit_s <= 0;
+  int64_t iter_cap = cfg_.iter_max;        // --time-limit lowers it
+  int64_t chunk_idx = 0, next_vote = 4;    // polled chunks; chunk of the next --time-limit vote
   const double watchdog = cfg_.watchdog_s;
   while (issued_ < iter_cap && !stop) {
     int64_t n = std::min(K, iter_cap - issued_);
@@ -1574,13 +1643,16 @@ RunResult Solver::run() {
         printed = hs.iter;
       }
       if (hs.done) stop = true;
-      // wall budget (--time-limit): turned into an iteration cap once, at the
-      // same chunk on every rank (a per-rank clock test could stop the ranks
-      // at different chunks, and the collectives would no longer pair up):
+      // wall budget (--time-limit): an iteration cap voted at the same chunk
+      // on every rank (a per-rank clock test could stop the ranks at
+      // different chunks, and the collectives would no longer pair up):
       // each rank projects the iterations that fit from its completed rate,
-      // the job takes the smallest (one all-reduce, in the collective order)
-      if (cfg_.time_limit_s > 0 && !capped && issued_ - iter0 >= 4 * K) {
-        capped = true;
+      // the job takes the smallest (one all-reduce, in the collective order).
+      // First after 4 chunks, then again every 8, so that a rate that drops
+      // later (clocks, contention) lowers the cap again.
+      ++chunk_idx;
+      if (cfg_.time_limit_s > 0 && chunk_idx >= next_vote) {
+        next_vote = chunk_idx + 8;
         const double el = now_s() - t0;
         const double rate = el > 0 ? (double)(hs.iter - iter0) / el : 0.0;
         int64_t cap = hs.iter + (int64_t)(rate * std::max(0.0, cfg_.time_limit_s - el));
@@ -1597,7 +1669,7 @@ RunResult Solver::run() {
           be_->release(d);
           cap = (int64_t)(big - v);
         }
-        iter_cap = std::max(issued_, std::min(iter_cap, cap));
+        iter_cap = std::max(issued_, std::min<int64_t>(cfg_.iter_max, cap));
       }
       if (cfg_.progress_s > 0 && is_root() && now_s() - last_beat >= cfg_.progress_s) {
         // heartbeat: long convergence runs (1024^3 at eps 1e-5: ~2e5

@@ -177,6 +177,13 @@ class Solver {
   // numbers describe the overlapped schedule as it runs.
   std::vector<std::pair<std::string, double>> profile_sweeps(int n);
 
+  // Link probe (the decomposition choice of a multi-GPU job): every rank
+  // exchanges `bytes` with each ring neighbour (ranks r - 1 and r + 1, the
+  // two x faces of a slab) at once, `reps` times after a warm-up, through the
+  // run's transport; returns the slowest rank's best one-way rate per link in
+  // GB/s (an all-reduce: the same value on every rank), 0 for one rank.
+  double link_probe(std::size_t bytes, int reps);
+
   // Race detection: compare order-independent checksums of every face sent
   // in the last exchange with the ghost layer the neighbour received.
   // Returns the number of mismatching faces (0 = consistent).
@@ -390,6 +397,10 @@ inline RcclOptions rccl_options(const Config& c) {
   RcclOptions o;
   o.shared = c.rccl_shared;
   o.graph = c.rccl_graph;
+  // the P2P kernels' blocks fit the CUs the compute stream leaves free
+  o.p2p_channels = c.rccl_p2p_channels > 0    ? c.rccl_p2p_channels
+                   : c.rccl_p2p_channels == 0 ? (c.reserve_cus > 0 ? c.reserve_cus : 8)
+                                              : 0;
   return o;
 }
 inline PhantomOptions phantom_options(const Config& c) {

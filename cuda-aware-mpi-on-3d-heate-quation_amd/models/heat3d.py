@@ -91,7 +91,7 @@ class HeatSolver:
                  dtype: str = "fp64", backend: str = "auto", comm: str = "auto",
                  decomp: Optional[Sequence[int]] = None, virtual_ranks: int = 1,
                  kernel: str = "auto", graph: bool = True, overlap: bool = True,
-                 check_every: int = 64, graph_chunk: int = 32, device: Optional[int] = None,
+                 check_every: int = 64, graph_chunk: int = 0, device: Optional[int] = None,
                  threads: int = 0, extra_args: Sequence[str] = (), group=None,
                  phantom: Optional[Sequence[int]] = None):
         ext = native()

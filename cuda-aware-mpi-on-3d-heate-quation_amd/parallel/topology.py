@@ -147,3 +147,27 @@ def best_dims_for(N: Sequence[int], nprocs: int, prefer: Optional[str] = None) -
     if (N[0] - 2) // nprocs >= 16:
         return (nprocs, 1, 1)
     return dims_create(nprocs)
+
+
+# Slab or 2D blocks for a multi-GPU job, from the measured link rate.  The
+# reference picks its process grid from the rank count alone
+# (MPI_Dims_create, heat3D.cu:243-263).  Phantom-rank proxy of the 1024^3 fp64
+# bench at the driver's window (profiles/rank_proxy_r04.md, emulated links):
+# 8 ranks as 8x1x1 slabs win from ~55 GB/s per link up (0.2179 vs 0.2377
+# ms/step at 96 GB/s), 4x2x1 blocks below (0.2603 vs 0.3256 at 32 GB/s),
+# because a slab sends 2 K-deep 1024^2 faces per sweep over one link each
+# while 4x2x1 sends 3 smaller ones; 4 ranks keep 4x1x1 at 40-64 GB/s
+# (0.4152 vs 0.4239 for 2x2x1) and 2 ranks have nothing else.
+SLAB_MIN_LINK_GBPS = {8: 55.0}
+
+
+def choose_dims(N: Sequence[int], nprocs: int, link_gbps: Optional[float]) -> Tuple[int, int, int]:
+    """--decomp auto of the bench: slabs (best_dims_for) unless the job's
+    slowest measured link (Solver.link_probe, GB/s one way) is below the
+    proxy's crossover for this rank count, then the 2D block with the x
+    extent halved and 2 ranks along y."""
+    slab = best_dims_for(N, nprocs)
+    cut = SLAB_MIN_LINK_GBPS.get(nprocs)
+    if cut is None or link_gbps is None or link_gbps <= 0 or link_gbps >= cut or slab[0] != nprocs:
+        return slab
+    return (nprocs // 2, 2, 1)

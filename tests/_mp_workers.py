@@ -169,3 +169,23 @@ def native_socket_policy_worker(rank, world, port, outdir, n, eps, decomp):
             f.write(f"{r['conv_iter']}\n")
     dist.barrier()
     dist.destroy_process_group()
+
+
+def link_probe_worker(rank, world, port, outdir, nbytes):
+    """Solver.link_probe over the socket transport: each rank exchanges
+    `nbytes` with both ring neighbours; the job agrees on the slowest rate,
+    and bench.py's decomposition vote (choose_dims) follows from it."""
+    dist = _init(rank, world, port)
+    import json
+
+    import heat3d_amd
+    from heat3d_amd.parallel import choose_dims
+
+    s = heat3d_amd.HeatSolver((4 * world + 2, 8, 8), 1, 0.0, backend="cpu", decomp=(world, 1, 1), threads=1)
+    gbps = s.native.link_probe(nbytes, 3)
+    dims = choose_dims((1024, 1024, 1024), world, gbps)
+    assert s.native.verify_halos() == 0
+    with open(os.path.join(outdir, f"probe{rank}.json"), "w") as f:
+        json.dump({"gbps": gbps, "dims": list(dims)}, f)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -121,11 +121,13 @@ def test_bench_self_launch_socket(gpu, tmp_path):
 
 
 @pytest.mark.parametrize("world,decomp,schedule", [(2, (2, 1, 1), ["--no-overlap"]), (4, (2, 2, 1), ["--no-overlap"]),
-                                                   (2, (2, 1, 1), ["--graph-multistream"])])
+                                                   (2, (2, 1, 1), []), (3, (3, 1, 1), []),
+                                                   (4, (2, 2, 1), [])])
 def test_rccl_graph_bitwise(h3d, gpu, tmp_path, world, decomp, schedule):
     """RCCL send / recv groups and all-reduces recorded into hipGraphs
     (--rccl-graph, the default): the single-stream schedule, and the
-    overlapped three-stream schedule with --graph-multistream.  The ranks
+    overlapped three-stream schedule (one linear graph per stream, device-side
+    cross-stream waits; x slabs and 2D blocks).  The ranks
     replay graphs (graph_launches > 0), exit cleanly and give the field of
     the eager single-process solve bit for bit.  Reference per-iteration
     comm: heat3D.cu:619-641 (halo), 1062-1063 (reduction)."""

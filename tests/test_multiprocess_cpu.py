@@ -12,7 +12,7 @@ import pytest
 import torch.multiprocessing as mp
 
 from conftest import free_port
-from _mp_workers import native_socket_worker, torch_reference_worker
+from _mp_workers import link_probe_worker, native_socket_worker, torch_reference_worker
 
 
 def _spawn(fn, world, *args):
@@ -130,3 +130,17 @@ def test_remainder_policy_vote_across_processes(h3d, tmp_path, world, decomp):
     r1 = single.run()
     assert int(open(tmp_path / "result.txt").read().split()[0]) == r1["conv_iter"]
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_link_probe_vote(h3d, tmp_path, world):
+    """The bench's --decomp auto: every rank times a face exchange with both
+    ring neighbours (one peer for 2 ranks) over the job's transport and the
+    ranks agree on the slowest rate, so they choose the same process grid."""
+    import json
+
+    _spawn(link_probe_worker, world, str(tmp_path), 1 << 20)
+    res = [json.loads((tmp_path / f"probe{r}.json").read_text()) for r in range(world)]
+    assert all(r == res[0] for r in res), res
+    assert res[0]["gbps"] > 0
+    assert res[0]["dims"][0] * res[0]["dims"][1] * res[0]["dims"][2] == world

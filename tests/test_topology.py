@@ -95,3 +95,21 @@ def test_layout_alignment(ext):
             assert (L["sy"] * es) % 128 == 0
             assert L["sy"] >= L["zoff"] + n[2] + 1
             assert L["elems"] >= (n[0] + 2) * L["sx"]
+
+
+def test_choose_dims_from_link_rate():
+    """--decomp auto of the bench: slabs at or above the proxy's crossover
+    (8 ranks: 55 GB/s), 4x2x1 below it; other rank counts and an unknown
+    rate keep the slab (heat3D.cu:243-263 picks by rank count alone)."""
+    from heat3d_amd.parallel import SLAB_MIN_LINK_GBPS, choose_dims
+
+    N = (1024, 1024, 1024)
+    assert SLAB_MIN_LINK_GBPS[8] == 55.0
+    assert choose_dims(N, 8, 64.0) == (8, 1, 1)
+    assert choose_dims(N, 8, 55.0) == (8, 1, 1)
+    assert choose_dims(N, 8, 40.0) == (4, 2, 1)
+    assert choose_dims(N, 8, 3.5) == (4, 2, 1)
+    assert choose_dims(N, 8, None) == (8, 1, 1)
+    assert choose_dims(N, 4, 10.0) == (4, 1, 1)
+    assert choose_dims(N, 2, 1.0) == (2, 1, 1)
+    assert choose_dims((40, 1024, 1024), 8, 10.0) == (2, 2, 2)   # slabs too thin: dims_create

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Reproducer / check for hipGraph capture of the overlapped multi-stream schedule.
+"""Check of hipGraph replays of the overlapped multi-stream schedule.
 
+The overlapped schedules replay one linear graph per stream (compute, comm,
+reduce), each launched on its own stream, with device-side signal / wait
+kernels for the cross-stream dependencies (csrc/runtime/hip_backend.cpp).
 Runs the same solve twice on one GPU — eager (--no-graph) and graph-captured —
 with P virtual ranks (LocalComm: halo copies on the comm stream, boundary slabs
 on the comm stream, residual check on the reduce stream, interior on the
@@ -38,9 +41,7 @@ def main() -> int:
     N = (args.n,) * 3
 
     def solve(graph: bool):
-        # multi-stream schedules are graphs only on request (solver.cpp graphs_allowed)
-        kw = dict(dtype=args.dtype, backend="hip", decomp=dims, graph=graph, graph_chunk=36, device=0,
-                  extra_args=["--graph-multistream"])
+        kw = dict(dtype=args.dtype, backend="hip", decomp=dims, graph=graph, graph_chunk=36, device=0)
         if args.phantom:
             r, p = (int(v) for v in args.phantom.split("/"))
             s = HeatSolver(N, iter_max=1 << 30, eps=0.0, phantom=(r, p), **kw)
