@@ -117,10 +117,10 @@ struct TunedSchedule {
 };
 std::vector<TunedSchedule> tuned_schedules();
 // fp32 lean kernel on packed pairs of z columns (stencil_tbp.hip; spec tlK:2:…)
-void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream);
-bool lean_pair_supported(const KernelSpec& k);
+void stencil_lean_pair(DType t, const StencilParams& p, const KernelSpec& k, void* stream);
+bool lean_pair_supported(DType t, const KernelSpec& k);
 // z tile stride of the pair kernel for a box (host-side choice, stencil_tbp.hip)
-int pair_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L);
+int pair_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L, int esize);
 // Is the lean kernel variant that k resolves to for dtype t instantiated?
 bool lean_supported(DType t, const KernelSpec& k);
 // Any multi-step kind -> its kernel

@@ -96,9 +96,10 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
       return true;
     }
   }
-  if (sizeof(Real) == 4 && r.V == 2) {  // packed fp32 pairs (stencil_tbp.hip)
-    if (!p) return lean_pair_supported(k);
-    stencil_lean_pair(*p, k, s);
+  if (r.V == 2) {  // two columns per lane: packed fp32 / 16-byte fp64 pairs (stencil_tbp.hip)
+    const DType t = sizeof(Real) == 8 ? DType::F64 : DType::F32;
+    if (!p) return lean_pair_supported(t, k);
+    stencil_lean_pair(t, *p, k, s);
     return true;
   }
   if (r.V != 1 || r.WZ != 1) return false;  // one value per lane, one wave across z

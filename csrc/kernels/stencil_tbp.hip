@@ -1,5 +1,5 @@
-// heat3d-mi355x — K-step temporally blocked FTCS kernel for fp32 with packed
-// math ("tlK:2:…": two z columns per lane).
+// heat3d-mi355x — K-step temporally blocked FTCS kernel with two z columns
+// per lane ("tlK:2:…"): fp32 in packed math, fp64 in 16-byte pairs.
 //
 // Same contract and structure as the lean kernel (stencil_tbl.hip: T^n ring,
 // K stages one plane apart, edge rows through LDS once per step, mask-free
@@ -22,7 +22,23 @@
 // Fields, residuals and iteration counts are bitwise identical to the
 // single-step kernels: each element goes through kernels.hpp ftcs_update's
 // operation sequence (packed FMA is two correctly rounded fp32 FMAs), and the
-// residual is |T^{n+1} - T^n| in fp32 (resid_abs).
+// residual is |T^{n+1} - T^n| in the field's precision (resid_abs_r).
+//
+// fp64 pairs (round 5, opt-in: --kernel2 tl3:2).  The one-value-per-lane
+// fp64 tile (64 x 48 points, 16 waves of 3 rows, 112 of 128 VGPRs) loads 64
+// columns to store 58 — 5 of the 128-byte L2 lines per 58 columns — and its
+// sweep reads 1.36x the field from HBM (profiles/l2_reuse_r04.md).  A pair
+// lane doubles the tile's width to 128 columns (122 stored, 9 lines) with
+// 16-byte loads and stores and one wave shift per direction per pair.  A
+// pair of doubles is 4 VGPRs and K = 3 keeps 9 plane rows per tile row, so
+// only 4 rows per wave fit 8 waves x 256 VGPRs (227; 5 and 6 rows spill):
+// 128 x 32 tiles.  Measured (profiles/fp64_pairs_r05.md): bitwise equal to
+// the lean kernel; half its VMEM, LDS and SALU instructions and 0.95x its
+// VALU per point, but the same HBM reads (1.38x against 1.36x: the shorter
+// tiles lose in y what the wider ones gain in z) and 825 against 838 GLUPS
+// on 1022^3; faster alone on the 8-GPU slab share's 122-plane interior (744
+// against 711: 360 tiles are 1.45 rounds of 248 CUs, 450 are 1.81) but not
+// inside the overlapped schedule, so the lean kernel stays the default.
 #include <hip/hip_runtime.h>
 
 #include <array>
@@ -55,7 +71,8 @@ struct TBPArgs {
 
 namespace {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
+template <typename T>
+using vec2 = T __attribute__((ext_vector_type(2)));
 
 constexpr int gcd_p(int a, int b) { return b == 0 ? a : gcd_p(b, a % b); }
 constexpr int lcm_p(int a, int b) { return a / gcd_p(a, b) * b; }
@@ -65,24 +82,42 @@ __device__ __forceinline__ int sgpr(int v) { return __builtin_amdgcn_readfirstla
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t prs(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)0xffffffff, 0x00020000);
 }
-__device__ __forceinline__ f2 ld2(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
-  return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// a pair load: 8 bytes (fp32) or 16 bytes (fp64) per lane
+template <typename T>
+__device__ __forceinline__ vec2<T> ld2(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  if constexpr (sizeof(T) == 8)
+    return __builtin_bit_cast(vec2<T>, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+  else
+    return __builtin_bit_cast(vec2<T>, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
 // AUX = cache-policy bits of the output stores (0 = default, 2 = nt)
-template <int AUX>
-__device__ __forceinline__ void st2(f2 v, __amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(unsigned __attribute__((ext_vector_type(2))), v), r,
-                                        voff, soff, AUX);
+template <int AUX, typename T>
+__device__ __forceinline__ void st2(vec2<T> v, __amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  if constexpr (sizeof(T) == 8)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, AUX);
+  else
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, AUX);
 }
-template <int AUX>
-__device__ __forceinline__ void st1(float v, __amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, AUX);
+template <int AUX, typename T>
+__device__ __forceinline__ void st1(T v, __amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  if constexpr (sizeof(T) == 8)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, AUX);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, AUX);
 }
-__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+template <typename T>
+__device__ __forceinline__ vec2<T> fma2(vec2<T> a, vec2<T> b, vec2<T> c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
 
 // kernels.hpp ftcs_update on a pair, same operation order per element
-__device__ __forceinline__ f2 ftcs2(f2 c, f2 xm, f2 xp, f2 ym, f2 yp, f2 zm, f2 zp, f2 Dx, f2 Dy, f2 Dz) {
-  const f2 m2 = {-2.f, -2.f};
+template <typename T>
+__device__ __forceinline__ vec2<T> ftcs2(vec2<T> c, vec2<T> xm, vec2<T> xp, vec2<T> ym, vec2<T> yp, vec2<T> zm,
+                                         vec2<T> zp, vec2<T> Dx, vec2<T> Dy, vec2<T> Dz) {
+  typedef vec2<T> f2;
+  const f2 m2 = {T(-2), T(-2)};
   const f2 ax = fma2(m2, c, xp) + xm;
   const f2 ay = fma2(m2, c, yp) + ym;
   const f2 az = fma2(m2, c, zp) + zm;
@@ -99,10 +134,11 @@ __device__ __forceinline__ void static_for_p(Fn&& fn) {
 
 }  // namespace
 
-template <int R, int WY, int K, int Q, int AUX = 0>
-__global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__ in, float* __restrict__ out,
-                                                       TBPArgs g, float Dxs, float Dys, float Dzs,
+template <typename T, int R, int WY, int K, int Q, int AUX = 0>
+__global__ __launch_bounds__(64 * WY) void stencil_tbp(const T* __restrict__ in, T* __restrict__ out,
+                                                       TBPArgs g, T Dxs, T Dys, T Dzs,
                                                        unsigned long long* res, const int* done) {
+  typedef vec2<T> f2;
   static_assert(K >= 2 && K <= 6, "temporal depth");
   static_assert(Q == 3 || Q == 4, "T^n ring size");
   constexpr int TY = WY * R;
@@ -158,20 +194,27 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
   const int xf_lo = max(max(x0 + 2 * (K - 1), g.ulo + K - 1), g.blo[0] + K - 1);
   const int xf_hi = min(min(xlast, g.uhi - 1), g.bhi[0] + K - 2);
 
-  unsigned ybits = 0;
+  // row masks (uniform): bit r = row in the update range, R + r = stored
+  // row, 2R + sR + r = row counted at stage s (64-bit for tall 8-wave tiles)
+  using YMask = std::conditional_t<(2 * R + K * R <= 32), unsigned, unsigned long long>;
+  static_assert(2 * R + K * R <= 64, "row mask bits");
+  YMask ybits = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int row = yb + r, rp = wave * R + r;
-    if (row >= g.uylo && row < g.uyhi) ybits |= 1u << r;
-    if (rp >= K && rp < TY - K && row >= g.blo[1] && row < g.bhi[1]) ybits |= 1u << (R + r);
+    if (row >= g.uylo && row < g.uyhi) ybits |= YMask(1) << r;
+    if (rp >= K && rp < TY - K && row >= g.blo[1] && row < g.bhi[1]) ybits |= YMask(1) << (R + r);
 #pragma unroll
     for (int s = 0; s < K; ++s)
       if (row >= g.uylo && row < g.uyhi && rp >= s + 1 && rp < TY - s - 1 && row >= g.blo[1] - (K - 1 - s) &&
           row < g.bhi[1] + (K - 1 - s))
-        ybits |= 1u << (2 * R + s * R + r);
+        ybits |= YMask(1) << (2 * R + s * R + r);
   }
-  ybits = (unsigned)sgpr((int)ybits);
-  static_assert(2 * R + K * R <= 32, "row mask bits");
+  if constexpr (sizeof(YMask) == 4) {
+    ybits = (unsigned)sgpr((int)ybits);
+  } else {
+    ybits = ((YMask)(unsigned)sgpr((int)(ybits >> 32)) << 32) | (unsigned)sgpr((int)(unsigned)ybits);
+  }
 
   const bool zin0 = col0 >= g.uzlo && col0 < g.uzhi, zin1 = col1 >= g.uzlo && col1 < g.uzhi;
   const bool zst0 = j0 >= g.hl && j0 < g.hl + g.zs && col0 >= g.blo[2] && col0 < g.bhi[2];
@@ -180,33 +223,33 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
 
   auto yclamp = [&](int row) { return min(max(row, g.ylo_live), g.yhi_live); };
   const int ybc = yclamp(yb);
-  const float* __restrict__ inw = in + (g.origin + (int64_t)ybc * g.sy + c0);
-  float* __restrict__ outw = out + (g.origin + (int64_t)yb * g.sy + c0);
+  const T* __restrict__ inw = in + (g.origin + (int64_t)ybc * g.sy + c0);
+  T* __restrict__ outw = out + (g.origin + (int64_t)yb * g.sy + c0);
   int roff[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) roff[r] = sgpr((yclamp(yb + r) - ybc) * (int)g.sy * (int)sizeof(float));
-  const int sy_b = (int)g.sy * (int)sizeof(float);
-  const unsigned lane_b = (unsigned)lane * 8u;
+  for (int r = 0; r < R; ++r) roff[r] = sgpr((yclamp(yb + r) - ybc) * (int)g.sy * (int)sizeof(T));
+  const int sy_b = (int)g.sy * (int)sizeof(T);
+  const unsigned lane_b = (unsigned)lane * (unsigned)sizeof(f2);
   const f2 Dx = {Dxs, Dxs}, Dy = {Dys, Dys}, Dz = {Dzs, Dzs};
 
   f2 q[Q][R];         // T^n ring: plane p in slot (p - x0 + 1) mod Q
   f2 f[K - 1][3][R];  // F_{s+1}(p) in f[s][(p + s) mod 3]
-  f2 m[K];            // per-element residual maxima (fp32, widened at the end)
+  f2 m[K];            // per-element residual maxima (field precision, widened at the end)
   bool nan_seen = false;
 #pragma unroll
-  for (int s = 0; s < K; ++s) m[s] = f2{0.f, 0.f};
+  for (int s = 0; s < K; ++s) m[s] = f2{T(0), T(0)};
 #pragma unroll
   for (int s = 0; s < K - 1; ++s)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int r = 0; r < R; ++r) f[s][i][r] = f2{0.f, 0.f};
+      for (int r = 0; r < R; ++r) f[s][i][r] = f2{T(0), T(0)};
 
   auto load_plane = [&](int x, f2 (&d)[R]) {
     const int xc = min(max(x, g.xlo_live), g.xhi_live);
     const __amdgpu_buffer_rsrc_t rs = prs(inw + (int64_t)xc * sx);
 #pragma unroll
-    for (int r = 0; r < R; ++r) d[r] = ld2(rs, lane_b, roff[r]);
+    for (int r = 0; r < R; ++r) d[r] = ld2<T>(rs, lane_b, roff[r]);
   };
   constexpr int NPRE = Q == 3 ? 3 : Q - 1;
 #pragma unroll
@@ -248,13 +291,13 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
         const f2 yp = r == R - 1 ? hi : C[r + 1 < R ? r + 1 : 0];
         const f2 zm = {dpp_shr1z(c.y), c.x};
         const f2 zp = {c.y, dpp_shl1z(c.x)};
-        const f2 nv = ftcs2(c, M[r], P[r], ym, yp, zm, zp, Dx, Dy, Dz);
+        const f2 nv = ftcs2<T>(c, M[r], P[r], ym, yp, zm, zp, Dx, Dy, Dz);
         const f2 d = __builtin_elementwise_abs(nv - c);  // resid_abs_r per element
         bool upd = true, cnt = true, st = true;
         if constexpr (!FAST) {
-          upd = xin && ((ybits >> r) & 1u);
-          cnt = xcnt && ((ybits >> (2 * R + s * R + r)) & 1u);
-          st = xst && ((ybits >> (R + r)) & 1u);
+          upd = xin && ((ybits >> r) & 1);
+          cnt = xcnt && ((ybits >> (2 * R + s * R + r)) & 1);
+          st = xst && ((ybits >> (R + r)) & 1);
         }
         if (s < K - 1) {
           f2(&N)[R] = f[s < K - 1 ? s : 0][fw];
@@ -270,10 +313,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
           nan_seen |= (zst0 && nv.x != nv.x) || (zst1 && nv.y != nv.y);
           const __amdgpu_buffer_rsrc_t ro = prs(outw + (int64_t)p * sx);
           if (zst2) {
-            st2<AUX>(nv, ro, lane_b, r * sy_b);
+            st2<AUX, T>(nv, ro, lane_b, r * sy_b);
           } else {
-            if (zst0) st1<AUX>(nv.x, ro, lane_b, r * sy_b);
-            if (zst1) st1<AUX>(nv.y, ro, lane_b + 4u, r * sy_b);
+            if (zst0) st1<AUX, T>(nv.x, ro, lane_b, r * sy_b);
+            if (zst1) st1<AUX, T>(nv.y, ro, lane_b + (unsigned)sizeof(T), r * sy_b);
           }
         }
       }
@@ -310,34 +353,36 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const float* __restrict__
 }
 
 // Tile stride along z: 128 - 2K - 2 stored columns (tiles start on even
-// columns), or the largest multiple of 16 below it, which starts every tile's
-// stored strip on a 64-byte boundary (whole 64-B write segments at both
-// seams; 2049^3 fp32 1456 -> 1531 GLUPS with 112 instead of 120, round 3).
+// columns), or the largest multiple of a 64-byte line (16 fp32, 8 fp64)
+// below it, which starts every tile's stored strip on a 64-byte boundary
+// (whole 64-B write segments at both seams; 2049^3 fp32 1456 -> 1531 GLUPS
+// with 112 instead of 120, round 3).
 // The narrower stride can add a tile column, so — as lean_z_stride does for
 // fp64 — it is taken only where the tiling cost (tiling_cost), with that
 // gain, predicts a shorter sweep, and only for boxes of >= 500 x planes
 // (1022^3: 120 keeps 9 tile columns, 112 would add a 14-wide 10th: 1397 vs
 // 1294 GLUPS).
-static int pair_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L);
-int pair_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L) {
+static int pair_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L, int esize);
+static int pair_aligned_stride(int wide, int esize) { return wide & ~(64 / esize - 1); }
+int pair_z_stride(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L, int esize) {
   // memoised: every eager launch asks
   static std::mutex mu;
-  static std::map<std::array<int64_t, 8>, int> memo;
-  const std::array<int64_t, 8> key{nx, ny, nz, K, TY, slots, U, L};
+  static std::map<std::array<int64_t, 9>, int> memo;
+  const std::array<int64_t, 9> key{nx, ny, nz, K, TY, slots, U, L, esize};
   {
     std::lock_guard<std::mutex> lk(mu);
     auto it = memo.find(key);
     if (it != memo.end()) return it->second;
   }
-  const int zs = pair_z_stride_plan(nx, ny, nz, K, TY, slots, U, L);
+  const int zs = pair_z_stride_plan(nx, ny, nz, K, TY, slots, U, L, esize);
   std::lock_guard<std::mutex> lk(mu);
   memo[key] = zs;
   return zs;
 }
 
-static int pair_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L) {
+static int pair_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int L, int esize) {
   const int wide = 128 - 2 * K - 2;
-  const int aligned = wide & ~15;
+  const int aligned = pair_aligned_stride(wide, esize);
   if (aligned == wide || aligned <= 0 || nx < 500) return wide;
   const int64_t nyb = std::max<int64_t>(1, (ny + TY - 2 * K - 1) / (TY - 2 * K));
   auto cost = [&](int zs) {
@@ -349,14 +394,14 @@ static int pair_z_stride_plan(int64_t nx, int64_t ny, int64_t nz, int K, int TY,
   return cost(aligned) * kAlignedGain < cost(wide) ? aligned : wide;
 }
 
-template <int R, int WY, int K, int Q, int AUX = 0>
+template <typename T, int R, int WY, int K, int Q, int AUX = 0>
 static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   const Box& b = p.box;
   constexpr int TY = WY * R;
   const Layout& L = p.L;
-  HEAT3D_CHECK(L.esize == 4, "tl pair kernel: fp32 fields only");
+  HEAT3D_CHECK(L.esize == (int64_t)sizeof(T), "tl pair kernel: field element size " << L.esize);
   HEAT3D_CHECK(L.n[0] + 2 * L.gx < (1LL << 30) && L.n[1] + 2 * L.gy < (1LL << 30) &&
-                   L.sy * (int64_t)sizeof(float) * (R + 2 * L.gy + TY + 2 * K) < (1LL << 31),
+                   L.sy * (int64_t)sizeof(T) * (R + 2 * L.gy + TY + 2 * K) < (1LL << 31),
                "tl pair: extents exceed 32-bit tile coordinates");
   TBPArgs g;
   g.sx = L.sx;
@@ -377,7 +422,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   g.xhi_live = (int)(L.n[0] + L.gx - 1);
   g.ylo_live = (int)-L.gy;
   g.yhi_live = (int)(L.n[1] + L.gy - 1);
-  // first loaded column: lo - K rounded down to even (8-byte pairs; rows are
+  // first loaded column: lo - K rounded down to even (aligned pairs; rows are
   // 128-B aligned), so a tile's stored columns start K or K + 1 in
   const int c = (int)b.lo[2] - K;
   g.c00 = c - (c & 1);
@@ -385,16 +430,17 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   // the tail pad (layout.hpp: two rows + 1024 elements) covers the last
   // tile's overhang of at most 127 columns; the row starts zoff >= 32 before k = 0
   HEAT3D_CHECK(g.c00 >= -L.zoff, "tl pair: tile columns before the row start");
-  HEAT3D_CHECK(L.zoff % 2 == 0 && L.sy % 2 == 0 && L.origin % 2 == 0, "tl pair: rows not 8-byte aligned");
+  HEAT3D_CHECK(L.zoff % 2 == 0 && L.sy % 2 == 0 && L.origin % 2 == 0, "tl pair: rows not pair-aligned");
   HEAT3D_CHECK(g.uylo - 1 >= -L.gy && g.uyhi <= L.n[1] + L.gy && g.uylo <= b.lo[1] && g.uyhi >= b.hi[1] &&
                    g.uzlo - 1 >= -L.gz && g.uzhi <= L.n[2] + L.gz && g.uzlo <= b.lo[2] && g.uzhi >= b.hi[2],
                "tl pair: y/z update range outside the ghosted layout");
   HEAT3D_CHECK(g.ulo - 1 >= g.xlo_live && g.uhi <= g.xhi_live + 1 && g.ulo <= b.lo[0] && g.uhi >= b.hi[0],
                "tl pair: u range [" << g.ulo << "," << g.uhi << ") outside the ghosted layout");
   static const int slots =  // magic static: thread-safe under --gpus N
-      device_slots(reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q, AUX>), 64 * WY);
+      device_slots(reinterpret_cast<const void*>(&stencil_tbp<T, R, WY, K, Q, AUX>), 64 * WY);
   constexpr int U = Q == 4 ? 12 : 6;
-  const int ZS = ks.ZS > 0 ? ks.ZS : pair_z_stride(b.extent(0), b.extent(1), b.extent(2), K, TY, slots, U, ks.L);
+  const int ZS =
+      ks.ZS > 0 ? ks.ZS : pair_z_stride(b.extent(0), b.extent(1), b.extent(2), K, TY, slots, U, ks.L, (int)sizeof(T));
   HEAT3D_CHECK(ZS >= 2 && ZS % 2 == 0 && ZS <= 128 - 2 * K - 2,
                "tl pair: z stride " << ZS << " must be even and in [2, " << 128 - 2 * K - 2 << "]");
   constexpr int YS = TY - 2 * K;
@@ -410,7 +456,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(!p.state || p.slot + K <= kResidualSlots, "tl pair: residual slots " << p.slot << "+" << K);
   static const int spill = [] {
     hipFuncAttributes a{};
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q, AUX>)) == hipSuccess
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&stencil_tbp<T, R, WY, K, Q, AUX>)) == hipSuccess
                ? (int)a.localSizeBytes
                : 0;
   }();
@@ -428,20 +474,21 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
     ga.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
     const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
     HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl pair: bad block count " << nblocks);
-    hipLaunchKernelGGL((stencil_tbp<R, WY, K, Q, AUX>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
-                       static_cast<const float*>(p.in), static_cast<float*>(p.out), ga, (float)p.D[0], (float)p.D[1],
-                       (float)p.D[2], r, done);
+    hipLaunchKernelGGL((stencil_tbp<T, R, WY, K, Q, AUX>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
+                       static_cast<const T*>(p.in), static_cast<T*>(p.out), ga, (T)p.D[0], (T)p.D[1], (T)p.D[2], r,
+                       done);
     HIPK_CHECK(hipGetLastError());
   };
-  const void* kfn = reinterpret_cast<const void*>(&stencil_tbp<R, WY, K, Q, AUX>);
+  const void* kfn = reinterpret_cast<const void*>(&stencil_tbp<T, R, WY, K, Q, AUX>);
   if (ks.L == 0 && ks.ZS == 0) {
     const int64_t box[3] = {b.extent(0), b.extent(1), b.extent(2)};
     if (p.tune) {
       std::vector<int> zs_opts{ZS};
-      const int wide = 128 - 2 * K - 2, aligned = wide & ~15;
+      const int wide = 128 - 2 * K - 2, aligned = pair_aligned_stride(wide, (int)sizeof(T));
       for (int z : {wide, aligned})
         if (z > 0 && std::find(zs_opts.begin(), zs_opts.end(), z) == zs_opts.end()) zs_opts.push_back(z);
-      tune_schedule("tl-fp32-pair", kfn, box, slots, p.cu_reserved, U, zs_opts, s, fire);
+      tune_schedule(sizeof(T) == 8 ? "tl-fp64-pair" : "tl-fp32-pair", kfn, box, slots, p.cu_reserved, U, zs_opts, s,
+                    fire);
       return;
     }
     SchedChoice c;
@@ -456,38 +503,47 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
 }
 
 // p == nullptr: only report whether the variant k resolves to exists
+template <typename T>
 static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) {
-  const KernelSpec r = k.resolved(DType::F32);
+  const KernelSpec r = k.resolved(sizeof(T) == 8 ? DType::F64 : DType::F32);
   const int K = k.K, R = r.R, WY = r.WY, Q = r.NT;
   if (r.V != 2 || r.WZ != 1) return false;
-#define H3D_TBP(RR, YY, KK, QQ)                                \
-  if (R == RR && WY == YY && K == KK && Q == QQ && r.O <= 0) {  \
-    if (p) launch_tbp<RR, YY, KK, QQ>(*p, k, s);               \
-    return true;                                               \
+  // AA: the output stores' cache-policy bits (spec field 7; 0 = default,
+  // which a spec without the field, O <= 0, selects)
+#define H3D_TBP(RR, YY, KK, QQ, AA)                                                             \
+  if (R == RR && WY == YY && K == KK && Q == QQ && (r.O == (AA) || ((AA) == 0 && r.O <= 0))) {  \
+    if (p) launch_tbp<T, RR, YY, KK, QQ, (AA)>(*p, k, s);                                       \
+    return true;                                                                                \
   }
-  // output-store cache policy (spec field 7), default shape only
-#define H3D_TBPA(AA)                                                       \
-  if (R == 3 && WY == 16 && K == 3 && Q == 3 && r.O == (AA)) {             \
-    if (p) launch_tbp<3, 16, 3, 3, (AA)>(*p, k, s);                        \
-    return true;                                                           \
+  if constexpr (sizeof(T) == 4) {
+    // output-store cache policy (spec field 7), default shape only
+    H3D_TBP(3, 16, 3, 3, 2) H3D_TBP(3, 16, 3, 3, 3) H3D_TBP(3, 16, 3, 3, 17) H3D_TBP(3, 16, 3, 3, 19)
+    H3D_TBP(3, 16, 3, 3, 0) H3D_TBP(3, 16, 3, 4, 0) H3D_TBP(2, 16, 3, 3, 0) H3D_TBP(2, 16, 4, 3, 0)
+    H3D_TBP(2, 16, 4, 4, 0) H3D_TBP(3, 16, 4, 3, 0) H3D_TBP(2, 16, 2, 3, 0) H3D_TBP(3, 16, 2, 3, 0)
+  } else {
+    // fp64 pairs: 8 waves (<= 256 VGPRs, 2 waves per SIMD) of 4 rows at
+    // K = 3 (5 and 6 rows spill: a pair is 4 VGPRs and K = 3 holds 9 plane
+    // rows per tile row; 16 waves of 2 rows take 145 VGPRs and 192 KiB of
+    // LDS), K = 2 in 6 rows and K = 4 in 3 rows of 8 waves; nt stores (2) or
+    // default (0)
+    H3D_TBP(4, 8, 3, 3, 2) H3D_TBP(4, 8, 3, 3, 0) H3D_TBP(6, 8, 2, 3, 2)
+    H3D_TBP(3, 8, 4, 3, 2)
   }
-  H3D_TBPA(2) H3D_TBPA(3) H3D_TBPA(17) H3D_TBPA(19)
-#undef H3D_TBPA
-
-  H3D_TBP(3, 16, 3, 3) H3D_TBP(3, 16, 3, 4) H3D_TBP(2, 16, 3, 3) H3D_TBP(2, 16, 4, 3) H3D_TBP(2, 16, 4, 4)
-  H3D_TBP(3, 16, 4, 3) H3D_TBP(2, 16, 2, 3) H3D_TBP(3, 16, 2, 3)
 #undef H3D_TBP
   return false;
 }
 
-bool lean_pair_supported(const KernelSpec& k) { return run_tbp(nullptr, k, nullptr); }
+bool lean_pair_supported(DType t, const KernelSpec& k) {
+  return t == DType::F64 ? run_tbp<double>(nullptr, k, nullptr) : run_tbp<float>(nullptr, k, nullptr);
+}
 
-void stencil_lean_pair(const StencilParams& p, const KernelSpec& k, void* stream) {
+void stencil_lean_pair(DType t, const StencilParams& p, const KernelSpec& k, void* stream) {
   if (p.box.empty()) return;
-  if (!run_tbp(&p, k, S(stream))) {
-    const KernelSpec r = k.resolved(DType::F32);
+  const bool ok = t == DType::F64 ? run_tbp<double>(&p, k, S(stream)) : run_tbp<float>(&p, k, S(stream));
+  if (!ok) {
+    const KernelSpec r = k.resolved(t);
     HEAT3D_THROW("unsupported tl pair variant V=" << r.V << " R=" << r.R << " WY=" << r.WY << " K=" << k.K
-                                                  << " Q=" << r.NT);
+                                                  << " Q=" << r.NT << " O=" << r.O);
   }
 }
 

@@ -204,9 +204,10 @@ PYBIND11_MODULE(_heat3d, m) {
     }
     return out;
   });
-  m.def("pair_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U) {
-    return heat3d::hip::pair_z_stride(nx, ny, nz, K, TY, slots, U, 0);
-  });
+  m.def("pair_z_stride", [](int64_t nx, int64_t ny, int64_t nz, int K, int TY, int slots, int U, int esize) {
+    return heat3d::hip::pair_z_stride(nx, ny, nz, K, TY, slots, U, 0, esize);
+  }, py::arg("nx"), py::arg("ny"), py::arg("nz"), py::arg("K"), py::arg("TY"), py::arg("slots"), py::arg("U"),
+     py::arg("esize") = 4);
   // a kernel spec with its per-dtype defaults filled in, as the solver
   // launches it (tests/test_temporal_cpu.py)
   m.def("kernel_spec_resolved", [](const std::string& spec, const std::string& dtype) {

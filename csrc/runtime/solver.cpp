@@ -127,6 +127,12 @@ KernelSpec KernelSpec::resolved(DType t) const {
         r.R = 3;
         r.WY = 8;
       }
+      // fp64 pairs (V = 2, stencil_tbp.hip): 8 waves (<= 256 VGPRs) of 4 rows,
+      // 32 x 128 tiles (K = 2: 6 rows, K = 4: 3 rows)
+      if (f64 && r.V == 2 && r.R == 0 && r.WY == 0 && K <= 4) {
+        r.R = K == 2 ? 6 : K == 4 ? 3 : 4;
+        r.WY = 8;
+      }
       def(r.R, (f64 || r.V == 2) ? (K >= 4 ? 2 : 3) : (K == 4 ? 4 : 3));
       def(r.WZ, 1);
       def(r.WY, 16);
@@ -143,6 +149,7 @@ KernelSpec KernelSpec::resolved(DType t) const {
       // fp32 packed-pair default shape too: 1388 -> 1431 GLUPS at 1024^3, 1354
       // -> 1513 at 2049^3
       if (!f64 && r.O < 0 && r.V == 2 && K == 3 && r.R == 3 && r.WY == 16 && r.NT == 3) r.O = 2;
+      if (f64 && r.O < 0 && r.V == 2 && r.NT == 3) r.O = 2;
       if (f64 && r.O < 0 && r.V == 1 && r.NT == 3 &&
           ((K == 3 && r.R == 3 && r.WY == 16) || (K == 4 && r.R == 2 && r.WY == 16) ||
            (K == 4 && r.R == 3 && r.WY == 12) || (K == 2 && r.R == 5 && r.WY == 16)))
@@ -520,6 +527,7 @@ void Solver::initialize() {
       be_->init_field(dt_, p, kCompute);
     }
   }
+  sweep_costs_.clear();
   tune_schedules();
   calibrate_remainders();
   DeviceState hs;
@@ -623,7 +631,6 @@ KernelSpec Solver::spec_for_depth(int Kp) const {
 
 void Solver::calibrate_remainders() {
   long_rem_ = ~0u;
-  sweep_costs_.clear();
   for (bool& d : depth_set_) d = false;
   if (!tb_ || cfg_.long_sweeps == 0) {
     long_rem_ = 0;
@@ -1353,6 +1360,10 @@ int Solver::graph_len_for(int64_t n) const {
   const int chunk = cfg_.graph_chunk > 0 ? cfg_.graph_chunk : multi_stream() ? 96 : 32;
   int G = std::max(cyc, chunk - chunk % cyc);
   if (n < G) G = (int)(n - n % cyc);
+  // a step count shorter than one cycle (the driver's 20-step window at 8
+  // ranks: 12 steps in K = 3 sweeps + 2 long sweeps; the 3-buffer cycle is
+  // 18) is one graph too, replayable only from the same state
+  if (G == 0 && tb_) G = (int)(n - n % K_);
   return G;
 }
 

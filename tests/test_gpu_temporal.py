@@ -109,11 +109,15 @@ VARIANTS_K = {3: ["tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5
                   "tl4:1:6:1:8:0:3", "tl4:1:6:1:8:0:4", "tl4:1:5:1:8:0:3", "tl4:1:6:1:8:7:3",
                   "tl4:1:3:1:12:0:3:2", "tl4:1:3:1:12:0:3"],
               2: ["tl2", "tl2:1:2:1:16:0:3", "tl2:1:5:1:16:0:3:2"]}
-# fp32 only: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)
+# fp32: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)
 PAIR = {3: ["tl3:2:3:1:16:0:3", "tl3:2:3:1:16:0:3:2", "tl3:2:3:1:16:0:4", "tl3:2:2:1:16:0:3", "tl3:2:3:1:16:5:3"],
         4: ["tl4:2:2:1:16:0:3", "tl4:2:2:1:16:0:4", "tl4:2:2:1:16:7:3"],
         2: ["tl2:2:2:1:16:0:3", "tl2:2:3:1:16:0:3"]}
 VARIANTS_K_F32 = PAIR
+# fp64: the same kernel with 16-byte pairs (8 waves; round 5)
+PAIR_F64 = {3: ["tl3:2", "tl3:2:4:1:8:0:3:0", "tl3:2:4:1:8:5:3:2"],
+            4: ["tl4:2", "tl4:2:3:1:8:7:3:2"],
+            2: ["tl2:2", "tl2:2:6:1:8:0:3:2"]}
 
 
 @pytest.mark.parametrize("K", [2, 3, 4])
@@ -131,7 +135,7 @@ def test_stencil_k_bitwise(h3d, gpu, K, dtype, n):
         T[1:-1, 1:-1, 1:-1] = u
         refs.append(r)
     want = T[1:-1, 1:-1, 1:-1]
-    for v in VARIANTS_K[K] + (VARIANTS_K_F32[K] if dtype == torch.float32 else []):
+    for v in VARIANTS_K[K] + (VARIANTS_K_F32[K] if dtype == torch.float32 else PAIR_F64[K]):
         out = ops.PaddedField(n, dtype=dtype, device=gpu)
         out.flat.fill_(-3.0)
         st = ops.new_state(gpu)
@@ -570,10 +574,10 @@ def test_remainder_policy_measured_gpu(h3d, gpu, vr, dims):
     # fp64 K = 2: both tile shapes timed, the partial sweep costs the faster one
     shapes = [k for k in costs if k.startswith("sweep2[")]
     assert len(shapes) == 2 and costs["sweep2"] == min(costs[k] for k in shapes), costs
+    t4 = costs["sweep4"]
     rem = a.native.long_remainders
     for r in (1, 2):
-        assert (r in rem) == (r * (costs["sweep4"] - costs["sweep3"]) < costs["step" if r == 1 else "sweep2"]), \
-            (rem, costs)
+        assert (r in rem) == (r * (t4 - costs["sweep3"]) < costs["step" if r == 1 else "sweep2"]), (rem, costs)
     for k in (5, 20, 7):
         a.step(k)
         b.step(k)

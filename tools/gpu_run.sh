@@ -23,6 +23,7 @@
 #   pmc VARIANT [N] [DTYPE] tools/pmc_passes.sh (one counter group per run) -> OUT/pmc<i>/
 #   py SCRIPT [ARGS]        any python script                              -> OUT/py<i>.log
 #   sh COMMAND...           a shell command (keep GPU work under its own timeout)
+#   env VAR=VALUE ...       export for the later steps
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -108,6 +109,8 @@ for step in "$@"; do
       tail -20 "$OUT/py$i.log" ;;
     sh)
       bash -c "${args[*]}" || fail sh $? ;;
+    env)
+      export "${args[@]}" ;;
     *)
       echo "unknown step '$name'"; exit 2 ;;
   esac
