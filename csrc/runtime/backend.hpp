@@ -76,11 +76,15 @@ class Backend {
   //     priority kept); a wait on an event another stream recorded inside
   //     the recording becomes a device-side wait on a signal slot, set by
   //     the recording stream (kernels graph_signal / graph_wait).  A wait
-  //     that times out marks `fault_state` (fault = 2, done = 1).
+  //     that times out (set_graph_wait_timeout) marks `fault_state`
+  //     (fault = 2, done = 1).
   // launch_graph joins every stream into the compute stream afterwards.
   virtual bool supports_graphs() const { return false; }
   virtual void begin_capture(bool /*per_stream*/ = false, DeviceState* /*fault_state*/ = nullptr,
                              int /*max_signals*/ = 0) {}
+  // how long a device-side wait of a per-stream graph may spin before it
+  // flags the fault (s; the solver passes its --watchdog)
+  virtual void set_graph_wait_timeout(double /*seconds*/) {}
   virtual void* end_capture() { return nullptr; }  // returns executable graph
   virtual void launch_graph(void* /*exec*/) {}
   virtual void destroy_graph(void* /*exec*/) {}

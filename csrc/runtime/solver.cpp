@@ -260,6 +260,7 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     slot_stride_ = K_ + (long_halo_ ? 1 : 0);
   }
   fake_allreduce_us_ = cfg_.fake_allreduce_us;
+  be_->set_graph_wait_timeout(cfg_.watchdog_s);
   chain_ = comm_->ordered_collectives() && !comm_->all_local() && comm_->size() > 1;
   // CU reservation for the overlapped schedule of a real multi-rank job
   // (RCCL or its phantom): the comm / boundary / check kernels must not queue
@@ -1720,6 +1721,8 @@ RunResult Solver::run() {
       if (it % cfg_.verbose == 0 && it >= hs.iter - hstate_->hist_cap)
         std::printf("iteration %lld residual %.6e\n", (long long)it, hstate_->hist[it % hstate_->hist_cap]);
   }
+  HEAT3D_CHECK(hs.fault != 2, "a device-side wait of a per-stream hipGraph timed out after "
+                                   << cfg_.watchdog_s << " s (broken dependency or a stalled peer)");
   R.seconds = t1 - t0;
   R.fault = hs.fault != 0;
   R.converged = hs.done && !hs.fault;
