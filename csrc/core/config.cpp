@@ -108,8 +108,6 @@ std::string Config::usage() {
      << "  --progress S              stderr heartbeat (iteration, residual, rate) every S seconds of run()\n"
      << "  --time-limit S            run(): stop (not converged) after about S seconds (0 = no limit)\n"
      << "  --threads N               CPU backend OpenMP threads\n"
-     << "  --boundary-stream auto|comm|compute  overlapped sweeps: boundary pieces beside the interior (comm\n"
-     << "                            stream, behind the halo) or after it on the compute stream\n"
      << "  --thin-layers             overlapped block sweeps: K-thick y / z boundary layers (default: one\n"
      << "                            tile stride thick, so that their tiles are not mostly halo)\n"
      << "  --reserve-cus N           CUs kept free of the interior sweep for comm / boundary / check\n"
@@ -248,13 +246,9 @@ Config Config::parse(int argc, const char* const* argv) {
       throw UsageError(key + " was retired in round 5 (measured slower on every configuration, "
                              "profiles/rank_proxy_r04.md)");
     else if (key == "--thin-layers") c.tile_layers = false;
-    else if (key == "--boundary-stream") {
-      const std::string v = get("--boundary-stream");
-      if (v == "auto") c.boundary_stream = -1;
-      else if (v == "comm") c.boundary_stream = 0;
-      else if (v == "compute") c.boundary_stream = 1;
-      else throw UsageError("--boundary-stream auto|comm|compute");
-    }
+    else if (key == "--boundary-stream")
+      throw UsageError("--boundary-stream was retired in round 5 (the boundary pieces run beside the interior "
+                       "on the comm stream; after it was slower on every configuration, profiles/r05/proxy_runs.md)");
     else if (key == "--long-sweeps") {
       const std::string v = get("--long-sweeps");
       if (v == "auto") c.long_sweeps = -1;

@@ -72,11 +72,6 @@ struct Config {
   // overlapped block sweeps: y / z boundary layers one tile stride thick
   // (whole tiles instead of K-thin ones; --thin-layers: K thick)
   bool tile_layers = true;
-  // overlapped sweeps: where the boundary pieces run.  comm: behind the halo
-  // on the comm stream, beside the interior; compute: after the interior on
-  // the compute stream (no contention for CUs; the halo still overlaps the
-  // interior).  -1 auto
-  int boundary_stream = -1;       // -1 auto, 0 comm, 1 compute
   bool quiet = false;
   int cpu_threads = 0;
   int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules

@@ -720,7 +720,6 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("field_buffers", &Solver::field_buffers)
       .def_property_readonly("ghost_depth", &Solver::ghost_depth)
       .def_property_readonly("long_halo_sweeps", &Solver::long_halo_sweeps)
-      .def_property_readonly("boundary_on_compute", &Solver::boundary_on_compute)
       .def("sweep_pieces", &Solver::sweep_pieces, py::arg("local") = 0)
       .def_property_readonly("long_remainders",
                              [](const Solver& s) {

@@ -350,9 +350,6 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     local_.push_back(l);
   }
   setup_faces();
-  // boundary pieces on the compute stream, after the interior: explicit only
-  // for now (auto = the comm stream)
-  bcomp_ = tb_overlap_ && cfg_.boundary_stream == 1;
   dstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
   hstate_ = static_cast<DeviceState*>(be_->alloc_host(2 * sizeof(DeviceState)));
   std::memset(hstate_, 0, 2 * sizeof(DeviceState));
@@ -1104,7 +1101,7 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   // (a long sweep right after a K-thick one, e.g. across step() calls)
   if (last_bnd_ > 0 && (dv ? K_ + 1 : K_) > last_bnd_) ev_wait(kComm, EV_INT + (q ^ 1));
   last_bnd_ = lb ? K_ + 1 : K_;
-  const StreamId sb = bnd_stream();
+  const StreamId sb = kComm;
   auto boundary_boxes = [&](Local& l) -> const std::vector<Box>& { return lb ? l.tb_boundary_long : l.tb_boundary; };
   // thin x-slab boundary pieces keep the y-marching thin-slab tiles whatever
   // tile shape --kernel2 gives the interior (the shape fields pick the form)
@@ -1114,11 +1111,7 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
     t.V = t.R = t.WZ = t.WY = t.NT = t.L = t.ZS = 0;
     return t;
   };
-  // (boundary pieces on the compute stream: the halo sends what the previous
-  // ones wrote there; EV_HALO marks the halo landed)
-  if (bcomp_) ev_wait(kComm, EV_BND + (q ^ 1));
   enqueue_halo(bi, kComm, dv);
-  if (bcomp_) ev_record(EV_HALO, kComm);
   flush_pending_reduce();
   // [A] interior planes: they read the planes the previous sweep's boundary
   // slabs wrote.  (Round 4's core/rim split, a core that did not wait for
@@ -1132,14 +1125,13 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   prof_record(prof_idx_, PE_INT1, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
-  // [B2] the boundary slabs, behind the halo on the comm stream (or behind
-  // the interior and the halo on the compute stream)
-  if (bcomp_) {
-    ev_wait(kCompute, EV_HALO);
-  } else {
-    ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
-    ev_wait(kComm, EV_CHK + chk_prev);
-  }
+  // [B2] the boundary slabs, behind the halo on the comm stream.  (Round 4's
+  // opt-in alternative, the boundary pieces after the interior on the
+  // compute stream, was removed in round 5: config 5's share ran 6.97
+  // against 6.65 ms/step with it, the 8-GPU slab share 0.231 against 0.209;
+  // profiles/r05/proxy_runs.md.)
+  ev_wait(kComm, EV_INT + (q ^ 1));  // previous interior read the planes we overwrite
+  ev_wait(kComm, EV_CHK + chk_prev);
   be_->range_push("boundary");
   prof_record(prof_idx_, PE_BND0, sb);
   for (auto& l : local_)
@@ -1175,7 +1167,7 @@ void Solver::flush_pending_reduce() {
   if (!pending_.valid) return;
   pending_.valid = false;
   const int q = pending_.q;
-  const StreamId sr = red_stream();
+  const StreamId sr = kReduce;
   ev_wait(sr, EV_INT + q);
   ev_wait(sr, EV_BND + q);
   prof_record(pending_.prof, PE_RED0, sr);

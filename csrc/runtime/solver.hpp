@@ -130,7 +130,6 @@ class Solver {
   // long sweeps cross the halos) and whether they do
   std::array<int64_t, 3> ghost_depth() const { return {hd_[0], hd_[1], hd_[2]}; }
   bool long_halo_sweeps() const { return long_halo_; }
-  int boundary_on_compute() const { return bcomp_ ? 1 : 0; }
   // the overlapped sweeps' interior and boundary pieces of local subdomain i
   // (lo0, hi0, lo1, hi1, lo2, hi2 each)
   std::vector<std::array<int64_t, 6>> sweep_pieces(int i) const {
@@ -309,10 +308,6 @@ class Solver {
   std::vector<std::pair<std::string, double>> sweep_costs_;  // start-up timings (ms per sweep)
   void calibrate_remainders();
   int last_bnd_ = 0;          // boundary-layer depth of the last overlapped sweep (0: none pending)
-  StreamId red_stream() const { return kReduce; }
-  StreamId bnd_stream() const { return bcomp_ ? kCompute : kComm; }
-  // boundary pieces after the interior on the compute stream (--boundary-stream)
-  bool bcomp_ = false;
   bool ordered_halo_ = false; // axis-ordered exchange filling edges / corners (deep y / z halos)
   int last_kind_ = 0;         // 1 = single step, 2 = pair: last enqueued schedule
   DType dt_;
@@ -343,10 +338,9 @@ class Solver {
   std::vector<Segment> segs_;       // ring of recent segments (for convergence rollback)
   std::size_t seg_head_ = 0;
 
-  // events: 0..1 int[p], 2..3 bnd[p], 4..5 check[p], 6 fork, 7 join comm, 8 join red, 9..10 poll,
-  // EV_HALO: the latest sweep's halo landed (comm stream; --boundary-stream compute)
+  // events: 0..1 int[p], 2..3 bnd[p], 4..5 check[p], 6 fork, 7 join comm, 8 join red, 9..10 poll
   enum { EV_INT = 0, EV_BND = 2, EV_CHK = 4, EV_FORK = 6, EV_JCOMM = 7, EV_JRED = 8, EV_POLL = 9,
-         EV_T0 = 11, EV_T1 = 12, EV_TOKEN = 13, EV_HALO = 14, EV_COUNT = 16 };
+         EV_T0 = 11, EV_T1 = 12, EV_TOKEN = 13, EV_COUNT = 16 };
   bool chain_ = false;              // collective ordering chain active
   struct PendingReduce {
     bool valid = false;

@@ -497,15 +497,14 @@ def test_preheat_keeps_rollback_input_gpu(h3d, gpu, vr, dims):
 
 
 @pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (8, 1, 1)), (8, (2, 2, 2)), (4, (1, 2, 2))])
-@pytest.mark.parametrize("dtype,bcomp", [("fp64", False), ("fp32", False), ("fp64", True)])
-def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype, bcomp):
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype):
     """The driver's window at N > 1 (warm-up 5, then 20 steps = 4 x 3 + 2 x 4):
     long K+1 sweeps across the halos, including the (K+1)-plane boundary
-    slabs (y-marching K = 4 thin-slab tiles), bitwise equal to single steps;
-    also with the boundary pieces on the compute stream."""
+    slabs (y-marching K = 4 thin-slab tiles), bitwise equal to single steps."""
     n = (82, 70, 150)
     a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims,
-                       extra_args=["--long-sweeps", "on"] + (["--boundary-stream", "compute"] if bcomp else []))
+                       extra_args=["--long-sweeps", "on"])
     b = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
     assert a.native.long_halo_sweeps
     a.initialize(), b.initialize()
@@ -521,15 +520,12 @@ def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype, bcomp):
 
 @pytest.mark.parametrize("vr,dims,n", [(8, (2, 2, 2), (82, 180, 260)), (4, (1, 2, 2), (40, 180, 380)),
                                         (4, (2, 2, 1), (90, 180, 100))])
-@pytest.mark.parametrize("dtype,thin,bcomp", [("fp64", False, False), ("fp32", False, False), ("fp64", True, False),
-                                              ("fp64", False, True), ("fp32", False, True)])
-def test_tile_thick_block_layers_gpu(h3d, gpu, vr, dims, n, dtype, thin, bcomp):
+@pytest.mark.parametrize("dtype,thin", [("fp64", False), ("fp32", False), ("fp64", True)])
+def test_tile_thick_block_layers_gpu(h3d, gpu, vr, dims, n, dtype, thin):
     """Overlapped block sweeps with y / z boundary layers one tile stride
-    thick (whole tiles; --thin-layers: K thick) on the device streams, the
-    boundary pieces beside the interior or after it (--boundary-stream
-    compute): regular, partial and long sweeps bitwise equal to single steps."""
-    extra = (["--long-sweeps", "on"] + (["--thin-layers"] if thin else [])
-             + (["--boundary-stream", "compute"] if bcomp else []))
+    thick (whole tiles; --thin-layers: K thick) on the device streams:
+    regular, partial and long sweeps bitwise equal to single steps."""
+    extra = ["--long-sweeps", "on"] + (["--thin-layers"] if thin else [])
     a = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims, extra_args=extra)
     b = h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", extra_args=["--temporal", "1"])
     a.initialize(), b.initialize()

@@ -409,24 +409,6 @@ def test_long_sweeps_across_halos(h3d, vr, dims, K):
     assert a.native.verify_halos() == 0
 
 
-@pytest.mark.parametrize("vr,dims", [(3, (3, 1, 1)), (8, (2, 2, 2)), (4, (1, 2, 2))])
-@pytest.mark.parametrize("K", [2, 3])
-def test_boundary_on_compute_stream(h3d, vr, dims, K):
-    """--boundary-stream compute: the boundary pieces after the interior on
-    the compute stream (the halo waits for the previous ones there); regular,
-    partial and long sweeps bitwise equal to single steps."""
-    n = (33, 29, 31)
-    a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", virtual_ranks=vr, decomp=dims,
-                       extra_args=["--temporal", str(K), "--boundary-stream", "compute"])
-    b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="cpu", extra_args=T1)
-    assert a.native.boundary_on_compute == 1
-    a.initialize(), b.initialize()
-    for k in (5, 20, 7, 11, 4):
-        a.step(k)
-        b.step(k)
-        assert np.array_equal(a.gather(), b.gather()), (vr, dims, K, k)
-
-
 @pytest.mark.parametrize("thin", [False, True])
 def test_tile_thick_block_layers(h3d, thin):
     """Overlapped block sweeps: y / z boundary layers one tile stride thick
@@ -451,8 +433,9 @@ def test_tile_thick_block_layers(h3d, thin):
 
 def test_retired_schedule_flags(h3d):
     """Round 4's opt-in schedule variants that lost on every configuration
-    (core/rim interiors, chunked halos) are refused with a clear message."""
-    for flag in (["--core-rim"], ["--halo-chunks", "4"]):
+    (core/rim interiors, chunked halos, boundary pieces after the interior on
+    the compute stream) are refused with a clear message."""
+    for flag in (["--core-rim"], ["--halo-chunks", "4"], ["--boundary-stream", "compute"]):
         with pytest.raises(Exception, match="retired"):
             h3d.HeatSolver((40, 37, 31), 10, 0.0, backend="cpu", virtual_ranks=2, decomp=(2, 1, 1),
                            extra_args=["--temporal", "3", *flag])

@@ -4,8 +4,7 @@
 # unit tests, single domain, 8 virtual ranks with K = 3 sweeps + checkpoint,
 # restart, 4 socket-connected processes (2x2x1 blocks, deep halos), and the
 # round-4 / round-5 schedules: long K+1 sweeps across the halos (slabs and
-# blocks, partial remainders, rollback), boundary pieces on the compute
-# stream, tile-thick y / z layers, and 3 socket processes timing their sweeps
+# blocks, partial remainders, rollback), tile-thick y / z layers, and 3 socket processes timing their sweeps
 # and voting (remainder policy, --time-limit cap re-votes).
 # CPU only — sanitised GPU runs are not available on this pool.
 set -e
@@ -41,10 +40,10 @@ for c in "3x1x1 --temporal 3" "2x1x1 --temporal 2" "2x2x2 --temporal 3" "1x1x3 -
     --long-sweeps on --check-every 7 --output none > ls_$n.log 2>&1
   grep -q converged ls_$n.log
 done
-# boundary pieces after the interior on the compute stream, partial sweeps
+# partial remainder sweeps on 2x2x2 blocks
 timeout 300 "$B/heat3d" 33 29 31 100000 1e-4 --backend cpu --threads 2 --virtual-ranks 8 --decomp 2x2x2 \
-  --temporal 2 --boundary-stream compute --no-long-sweeps --output none > bcomp.log 2>&1
-grep -q converged bcomp.log
+  --temporal 2 --no-long-sweeps --output none > partial.log 2>&1
+grep -q converged partial.log
 # tile-thick y / z boundary layers (85 x 117 owned per rank)
 timeout 300 "$B/heat3d" 14 172 236 300 0 --backend cpu --threads 2 --virtual-ranks 4 --decomp 1x2x2 \
   --temporal 3 --output none > tile.log 2>&1
