@@ -58,3 +58,27 @@ def test_short_bench_replays_graph(h3d, gpu):
     s.synchronize()
     assert s.native.graph_launches - g0 == 1
     assert s.state()["iter"] == 25
+
+
+def test_stream_graph_wait_timeout_flags_fault(h3d, gpu):
+    """The safety net of the per-stream graphs: a device-side cross-stream
+    wait that outlasts --watchdog gives up, sets fault = 2 and the done flag
+    (later sweeps are no-ops) instead of holding the GPU.  A phantom rank
+    whose emulated halo takes ~3 s (a link of 4e-5 GB/s) makes the compute
+    stream's wait for the boundary slabs exceed a 0.5 s watchdog."""
+    import time
+
+    s = h3d.HeatSolver((64, 64, 64), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(1, 8),
+                       graph_chunk=6,
+                       extra_args=["--phantom-gbps", "4e-5", "--phantom-allreduce-us", "1", "--watchdog", "0.5",
+                                   "--long-sweeps", "off"])
+    s.initialize()
+    g0 = s.native.graph_launches
+    t0 = time.perf_counter()
+    s.step(6)   # one graph of two sweeps: the second interior waits for the first boundary slabs
+    s.synchronize()
+    el = time.perf_counter() - t0
+    assert s.native.graph_launches - g0 == 1
+    st = s.state()
+    assert st["fault"] == 2 and st["done"] == 1, st
+    assert el < 60, el   # the two emulated halos (~3 s each) end, nothing waits for ever
