@@ -520,8 +520,6 @@ static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) 
     H3D_TBP(3, 16, 3, 3, 2) H3D_TBP(3, 16, 3, 3, 3) H3D_TBP(3, 16, 3, 3, 17) H3D_TBP(3, 16, 3, 3, 19)
     H3D_TBP(3, 16, 3, 3, 0) H3D_TBP(3, 16, 3, 4, 0) H3D_TBP(2, 16, 3, 3, 0) H3D_TBP(2, 16, 4, 3, 0)
     H3D_TBP(2, 16, 4, 4, 0) H3D_TBP(3, 16, 4, 3, 0) H3D_TBP(2, 16, 2, 3, 0) H3D_TBP(3, 16, 2, 3, 0)
-    // 8 waves of 8 rows (<= 256 VGPRs): 64 x 128 tiles, 58 x 122 stored (1.16x against 1.22x)
-    H3D_TBP(8, 8, 3, 3, 2) H3D_TBP(8, 8, 3, 3, 0)
   } else {
     // fp64 pairs: 8 waves (<= 256 VGPRs, 2 waves per SIMD) of 4 rows at
     // K = 3 (5 and 6 rows spill: a pair is 4 VGPRs and K = 3 holds 9 plane
