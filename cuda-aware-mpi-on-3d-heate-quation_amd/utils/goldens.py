@@ -27,6 +27,9 @@ GOLDENS: Dict[Tuple[int, Optional[float]], Tuple[int, float, float]] = {
     # round 3: the native CPU backend (OpenMP, exact FMA; the definition every
     # GPU kernel is bitwise-tested against), 513^3 fp64, 270 s on 6 threads
     (513, 1e-3): (2132, 42.7695, 0.199740),
+    # round 5: the native CPU backend, 1024^3 fp64 (the headline grid), 3244 s
+    # on 6 threads (profiles/golden_1024_cpu_r05.log)
+    (1024, 1e-3): (2170, 46.2574, 0.199870),
 }
 # 27^3 with ITER_MAX = 100 (not converged): error 26.0129 %
 ITERMAX_100_27 = 26.0129
