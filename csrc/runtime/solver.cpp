@@ -680,10 +680,11 @@ void Solver::calibrate_remainders() {
     }
   };
   // candidates: the K and K+1 sweeps, a single step, the partial sweeps;
-  // fp64 K = 2 in two tile shapes: 80-row tiles (fewer halo rows per stored
-  // one, the kernel-level winner) and 48-row ones (a 122-plane slab share on
-  // 248 CUs takes 252 of the tall tiles = two rounds, 450 short ones also
-  // two: the short ones won there, 0.52 against 0.70 ms)
+  // fp64 K = 2 in three tile shapes: 80-row tiles (fewer halo rows per stored
+  // one), 48-row ones (a 122-plane slab share on 248 CUs takes 252 of the
+  // tall tiles = two rounds, 450 short ones also two: the short ones won
+  // there, 0.52 against 0.70 ms) and 48 x 128 pair tiles (stencil_tbp.hip:
+  // 624 against 584 GLUPS on 1022^3; a 1022^2 face is 216 of them, one round)
   struct Cand {
     int Kp;
     KernelSpec ks;
@@ -693,7 +694,7 @@ void Solver::calibrate_remainders() {
                           {K_ + 1, spec_for_depth(K_ + 1), "sweep" + std::to_string(K_ + 1)}};
   for (int r = 1; r < K_; ++r) {
     if (r == 2 && dt_ == DType::F64 && kspec2_.kind == KernelSpec::TBL && be_->is_gpu()) {
-      for (const char* v : {"tl2:1:5:1:16:0:3:2", "tl2:1:3:1:16:0:3:2"}) {
+      for (const char* v : {"tl2:1:5:1:16:0:3:2", "tl2:1:3:1:16:0:3:2", "tl2:2:6:1:8:0:3:2"}) {
         const KernelSpec ks = KernelSpec::parse(v);
         if (hip::lean_supported(dt_, ks)) cands.push_back({2, ks, std::string("sweep2[") + v + "]"});
       }

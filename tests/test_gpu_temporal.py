@@ -567,9 +567,10 @@ def test_remainder_policy_measured_gpu(h3d, gpu, vr, dims):
     a.initialize(), b.initialize()
     costs = a.native.sweep_costs
     assert {"sweep3", "sweep4", "step", "sweep2"} <= set(costs) and all(v > 0 for v in costs.values()), costs
-    # fp64 K = 2: both tile shapes timed, the partial sweep costs the faster one
+    # fp64 K = 2: three tile shapes timed (two lean, one pair), the partial
+    # sweep costs the fastest
     shapes = [k for k in costs if k.startswith("sweep2[")]
-    assert len(shapes) == 2 and costs["sweep2"] == min(costs[k] for k in shapes), costs
+    assert len(shapes) == 3 and costs["sweep2"] == min(costs[k] for k in shapes), costs
     t4 = costs["sweep4"]
     rem = a.native.long_remainders
     for r in (1, 2):
