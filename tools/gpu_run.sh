@@ -7,6 +7,9 @@
 # step that fails (GPU fault, abort, time limit) and runs nothing after it.
 # OUT is a directory under gpurun_out/ (created).  Steps:
 #
+#   build                   __graft_entry__.build() on the box (a fresh configure: the checkout
+#                           path differs from the one the shipped build/ was configured in)
+#                                                                          -> OUT/build.log
 #   suite [PYTEST ARGS]     python -m pytest -m gpu (default: tests/)       -> OUT/pytest.log
 #   smoke                   __graft_entry__.smoke()                        -> OUT/smoke.log
 #   bench [BENCH ARGS]      python bench.py ARGS (1 GPU, or --gpus N self-launch)
@@ -62,6 +65,10 @@ for step in "$@"; do
   args=("${a[@]:1}")
   echo "== step $i: $step"
   case "$name" in
+    build)
+      timeout -k 10 900 python3 -c "import __graft_entry__ as g; g.build()" > "$OUT/build$i.log" 2>&1 \
+        || { rc=$?; tail -30 "$OUT/build$i.log"; fail build $rc; }
+      tail -2 "$OUT/build$i.log" ;;
     suite)
       [ ${#args[@]} -eq 0 ] && args=(tests/)
       timeout -k 10 1000 python3 -u -m pytest -x -q --durations 8 --timeout 200 --timeout-method thread -m gpu \
