@@ -526,6 +526,12 @@ void Solver::initialize() {
     }
   }
   sweep_costs_.clear();
+  if (pick_sweep_form()) {  // re-timed from the lean form on every initialisation
+    KernelSpec lean;
+    lean.kind = kspec2_.kind;
+    lean.K = K_;
+    kspec2_ = lean;
+  }
   tune_schedules();
   calibrate_remainders();
   DeviceState hs;
@@ -574,6 +580,7 @@ void Solver::tune_schedules() {
   const bool on = cfg_.autotune > 0 || (cfg_.autotune < 0 && !has_halo_ && local_.size() == 1);
   if (!on || !tb_ || !be_->is_gpu()) return;
   std::vector<KernelSpec> specs{kspec2_};
+  if (pick_sweep_form()) specs.push_back(pair_form());
   if ((!has_halo_ || long_halo_) && cfg_.long_sweeps && K_ + 1 <= 6 && K_ + 1 <= kResidualSlots) {
     KernelSpec ks;
     ks.kind = kspec2_.kind;
@@ -625,6 +632,29 @@ KernelSpec Solver::spec_for_depth(int Kp) const {
   ks.kind = kspec2_.kind;
   ks.K = Kp;
   return ks;
+}
+
+// Sweep form of a single-subdomain fp64 run: the one-value-per-lane lean
+// kernel or its 16-byte pair form (stencil_tbp.hip), whichever the start-up
+// timing finds faster on this box.  Same box, driver window (1 GPU, 1024^3,
+// 20 / 5): pair 851.5-853.5 against lean 839.6-842.4 GLUPS, where the
+// kernel-level timing of round 5's first boxes had the pair form 1.5% slower
+// (profiles/fp64_pairs_r05.md).  Only where the sweeps run alone as timed;
+// under the overlapped multi-rank schedule the standalone timing picked the
+// pairs and they ran no faster there.
+bool Solver::pick_sweep_form() const {
+  if (!tb_ || !be_->is_gpu() || dt_ != DType::F64 || has_halo_ || local_.size() != 1 || cfg_.kernel2 != "auto" ||
+      kspec2_.kind != KernelSpec::TBL)
+    return false;
+  return hip::lean_supported(dt_, pair_form());
+}
+
+KernelSpec Solver::pair_form() const {
+  KernelSpec p;
+  p.kind = kspec2_.kind;
+  p.K = K_;
+  p.V = 2;
+  return p;
 }
 
 void Solver::calibrate_remainders() {
@@ -692,6 +722,14 @@ void Solver::calibrate_remainders() {
   };
   std::vector<Cand> cands{{K_, kspec2_, "sweep" + std::to_string(K_)},
                           {K_ + 1, spec_for_depth(K_ + 1), "sweep" + std::to_string(K_ + 1)}};
+  const bool pick_form = pick_sweep_form();
+  if (pick_form) {
+    cands.push_back({K_, pair_form(), "sweep" + std::to_string(K_) + "[" + pair_form().resolved(dt_).str() + "]"});
+    KernelSpec pl = pair_form();  // and the pair form of the long sweep
+    pl.K = K_ + 1;
+    if (hip::lean_supported(dt_, pl))
+      cands.push_back({K_ + 1, pl, "sweep" + std::to_string(K_ + 1) + "[" + pl.resolved(dt_).str() + "]"});
+  }
   for (int r = 1; r < K_; ++r) {
     if (r == 2 && dt_ == DType::F64 && kspec2_.kind == KernelSpec::TBL && be_->is_gpu()) {
       for (const char* v : {"tl2:1:5:1:16:0:3:2", "tl2:1:3:1:16:0:3:2", "tl2:2:6:1:8:0:3:2"}) {
@@ -737,6 +775,7 @@ void Solver::calibrate_remainders() {
         depth_spec_[Kp] = cands[c].ks;
         depth_set_[Kp] = true;
       }
+      if (Kp == K_ && pick_form) kspec2_ = cands[c].ks;  // the faster sweep form (pick_sweep_form)
     }
   }
   for (int Kp = 2; Kp < K_; ++Kp)

@@ -307,6 +307,8 @@ class Solver {
   KernelSpec spec_for_depth(int Kp) const;
   std::vector<std::pair<std::string, double>> sweep_costs_;  // start-up timings (ms per sweep)
   void calibrate_remainders();
+  bool pick_sweep_form() const;
+  KernelSpec pair_form() const;
   int last_bnd_ = 0;          // boundary-layer depth of the last overlapped sweep (0: none pending)
   bool ordered_halo_ = false; // axis-ordered exchange filling edges / corners (deep y / z halos)
   int last_kind_ = 0;         // 1 = single step, 2 = pair: last enqueued schedule
