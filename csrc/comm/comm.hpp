@@ -96,6 +96,10 @@ struct PhantomOptions {
   // time (an exchange lasts max(wire, copies)), as a transport that moves the
   // data while it is on the wire
   bool overlap_copies = false;
+  // paced: the copies themselves move the data at the wire rate, `channels`
+  // workgroups per transfer for the wire time (RCCL-like: a few channels
+  // stream the face across the link; no burst copy after the wire time)
+  bool paced = false;
 };
 std::unique_ptr<Comm> make_phantom_comm(int rank, int size, const PhantomOptions& o = {});
 

@@ -14,6 +14,8 @@
 // Collectives are ordered like RCCL's (ordered_collectives).  This is how the
 // per-GPU time of the multi-GPU bench is measured on the one-GPU box
 // (tools/rank_proxy.py).
+#include <algorithm>
+#include <cmath>
 #include <map>
 
 #include "comm.hpp"
@@ -26,7 +28,7 @@ class PhantomComm final : public Comm {
  public:
   PhantomComm(int rank, int size, const PhantomOptions& o)
       : rank_(rank), size_(size), gbps_(o.gbps), ar_us_(o.allreduce_us), channels_(o.channels),
-        ar_channels_(o.allreduce_channels), overlap_(o.overlap_copies) {
+        ar_channels_(o.allreduce_channels), overlap_(o.overlap_copies), paced_(o.paced) {
     HEAT3D_CHECK(rank >= 0 && rank < size, "phantom rank " << rank << " of " << size);
   }
   ~PhantomComm() override {
@@ -48,6 +50,27 @@ class PhantomComm final : public Comm {
     // bytes / (GB/s) in us, every peer's channels in flight at once
     const double wire = worst && gbps_ > 0 ? worst / (gbps_ * 1e3) : 0.0;
     const int blocks = channels_ * (int)per_peer.size();
+    if (paced_ && wire > 0) {
+      // every transfer from peer p ends bytes(p) / gbps after it starts
+      // workgroups per transfer: the channels, and enough that none must
+      // stream more than ~2 GB/s (at 4 GB/s per 256-lane group, four 16-byte
+      // loads in flight per lane, the 64 GB/s wire ran 9-17 % long beside
+      // the interior sweep: gpurun_out/r7m/proxytrace11)
+      const int per = std::max(channels_, (int)std::ceil(gbps_ / 2.0));
+      std::vector<hip::PacedCopy> pc;
+      for (const auto& x : xs) {
+        if (x.dst_rank != rank_ || x.src_rank == rank_) continue;
+        const void* src = nullptr;
+        for (const auto& y : xs)
+          if (y.src_rank == rank_ && y.bytes == x.bytes) src = y.src;
+        if (!src) continue;
+        const double peer_ticks = per_peer[x.src_rank] / (gbps_ * 1e3) * 100.0;  // 100 MHz clock
+        const double share16 = std::max(1.0, std::ceil((double)(x.bytes / 16) / per));
+        pc.push_back({src, x.dst, (int64_t)x.bytes, peer_ticks / share16});
+      }
+      be.paced_copy(pc, per, s);
+      return;
+    }
     // one clock stamp per stream: exchanges queued on different streams
     // (single-step halos, overlapped sweeps) must not share the stamp an
     // earlier delay_since still reads
@@ -82,7 +105,7 @@ class PhantomComm final : public Comm {
   int rank_, size_;
   double gbps_, ar_us_;
   int channels_, ar_channels_;
-  bool overlap_;
+  bool overlap_, paced_;
   Backend* be_ = nullptr;  // owner of slot_ (outlives the communicator, ~Solver)
   void* slot_ = nullptr;   // device clock stamps of the exchanges in flight, one per stream
 };

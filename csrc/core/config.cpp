@@ -135,7 +135,8 @@ std::string Config::usage() {
      << "  --fake-allreduce-us U     diagnostic: emulated all-reduce latency for virtual ranks\n"
      << "  --phantom-gbps G --phantom-allreduce-us U --phantom-channels C --phantom-allreduce-channels C\n"
      << "                            phantom-rank proxy (tools/rank_proxy.py) link emulation\n"
-     << "  --phantom-wire serial|overlap  phantom exchange: wire time then copies, or copies inside it\n"
+     << "  --phantom-wire serial|overlap|paced  phantom exchange: wire time then copies, copies inside it,\n"
+     << "                            or copies paced at the wire rate over the wire time\n"
      << "  --quiet                   suppress the banner\n";
   return os.str();
 }
@@ -280,8 +281,9 @@ Config Config::parse(int argc, const char* const* argv) {
     else if (key == "--phantom-gbps") c.phantom_gbps = to_f64(get("--phantom-gbps"), "--phantom-gbps");
     else if (key == "--phantom-wire") {
       const std::string v = get("--phantom-wire");
-      if (v != "serial" && v != "overlap") throw UsageError("--phantom-wire serial|overlap");
+      if (v != "serial" && v != "overlap" && v != "paced") throw UsageError("--phantom-wire serial|overlap|paced");
       c.phantom_overlap = v == "overlap";
+      c.phantom_paced = v == "paced";
     }
     else if (key == "--phantom-allreduce-us")
       c.phantom_allreduce_us = to_f64(get("--phantom-allreduce-us"), "--phantom-allreduce-us");

@@ -135,6 +135,17 @@ void check_convergence(DeviceState* s, int slot, void* stream, int count = 1);
 void delay(double us, void* stream, int blocks = 1);
 void stamp(void* slot, void* stream);
 void delay_since(const void* slot, double us, void* stream, int blocks = 1);
+// a phantom transfer paced at the wire rate (phantom_comm.cpp, --phantom-wire
+// paced): 16-byte aligned, ticks of the 100 MHz clock per 16 bytes of one
+// workgroup's share
+struct PacedCopy {
+  const void* src = nullptr;
+  void* dst = nullptr;
+  int64_t bytes = 0;
+  double ticks_per16 = 0.0;
+};
+constexpr int kPacedMax = 8;  // transfers per launch
+void paced_copy(const PacedCopy* xs, int n, int per, void* stream);
 // placement probe: out[b] = XCC << 8 | SE/SH/CU id of workgroup b (blocks x 64 threads)
 void cu_probe(unsigned* out, int blocks, double us, void* stream);
 // Device-side stream dependencies of per-stream hipGraphs (hip_backend.cpp):

@@ -119,6 +119,10 @@ class Backend {
   // that ends `us` after the stamp (emulated transfers overlapping copies)
   virtual void stamp(void* /*slot*/, StreamId /*s*/) {}
   virtual void delay_since(const void* /*slot*/, double us, StreamId s, int blocks = 1) { delay(us, s, blocks); }
+  // transfers paced at a wire rate (phantom transport): plain copies by default
+  virtual void paced_copy(const std::vector<hip::PacedCopy>& xs, int /*per*/, StreamId s) {
+    for (const auto& x : xs) copy(x.dst, x.src, (std::size_t)x.bytes, CopyKind::D2D, s);
+  }
   // tracing ranges (roctx on HIP)
   virtual void range_push(const char* /*name*/) {}
   virtual void range_pop() {}

@@ -422,6 +422,10 @@ class HipBackend final : public Backend {
   }
   void delay(double us, StreamId s, int blocks) override { op(s, [&](hipStream_t st) { hip::delay(us, st, blocks); }); }
   void stamp(void* slot, StreamId s) override { op(s, [&](hipStream_t st) { hip::stamp(slot, st); }); }
+  void paced_copy(const std::vector<hip::PacedCopy>& xs, int per, StreamId s) override {
+    if (xs.empty()) return;
+    op(s, [&](hipStream_t st) { hip::paced_copy(xs.data(), (int)xs.size(), per, st); });
+  }
   void delay_since(const void* slot, double us, StreamId s, int blocks) override {
     op(s, [&](hipStream_t st) { hip::delay_since(slot, us, st, blocks); });
   }

@@ -405,6 +405,7 @@ inline PhantomOptions phantom_options(const Config& c) {
   o.allreduce_us = c.phantom_allreduce_us;
   o.channels = c.phantom_channels;
   o.overlap_copies = c.phantom_overlap;
+  o.paced = c.phantom_paced;
   o.allreduce_channels = c.phantom_allreduce_channels;
   return o;
 }

@@ -166,7 +166,7 @@ def test_phantom_rank_proxy_runs(h3d, rank, size, decomp, temporal):
     issued iteration accounted for, nothing converges at eps 0."""
     s = h3d.HeatSolver((20, 20, 20), 1 << 40, 0.0, backend="cpu", decomp=decomp, phantom=(rank, size),
                        threads=2, extra_args=["--temporal", temporal, "--phantom-allreduce-us", "0",
-                                              "--phantom-wire", "overlap" if rank % 2 else "serial"])
+                                              "--phantom-wire", ("serial", "overlap", "paced")[rank % 3]])
     assert s.native.comm_name == "phantom"
     s.initialize()
     s.step(13)

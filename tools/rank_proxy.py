@@ -35,9 +35,11 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--gbps", type=float, default=50.0, help="emulated halo bandwidth per peer (GB/s)")
     ap.add_argument("--ar-us", type=float, default=20.0, help="emulated all-reduce latency (us)")
-    ap.add_argument("--wire", default="serial", choices=["serial", "overlap"],
+    ap.add_argument("--wire", default="serial", choices=["serial", "overlap", "paced"],
                     help="serial: an exchange is bytes / gbps, then the stand-in D2D copies; overlap: the "
-                         "copies run inside the wire time (a transport moving data while on the wire)")
+                         "copies run inside the wire time (a transport moving data while on the wire); paced: "
+                         "the copies move the data at the wire rate over the wire time (RCCL-like channels, "
+                         "no burst)")
     ap.add_argument("--backend", default="hip")
     ap.add_argument("--extra", default="", help="extra solver flags, e.g. '--no-overlap'")
     ap.add_argument("--preheat-ms", type=float, default=0.0,
