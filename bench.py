@@ -74,6 +74,9 @@ def parse_args(argv=None):
                     help="wall budget (s) of the time-to-converge run: past it the run stops unconverged and "
                          "the JSON says so (bounds the driver's bench on a slow box; 0 = none)")
     ap.add_argument("--temporal", type=int, default=0, help="0 auto | 1 single-step | K (2..6) K-step temporally blocked sweeps")
+    ap.add_argument("--reserve-cus", type=int, default=-1,
+                    help="CUs kept free of the interior sweep for the comm kernels (-1 auto: 8 under the "
+                         "overlapped multi-rank schedule, 0 under a long x-slab interior)")
     ap.add_argument("--kernel2", default="auto", help="temporally blocked sweep kernel (tbK / trK[:V:R:WZ:WY:L:Q])")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: split the grid into this many subdomains on one GPU (not the headline)")
@@ -237,7 +240,8 @@ def run_rank(args) -> int:
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
                           device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
                           extra_args=["--temporal", str(args.temporal), "--kernel2", args.kernel2,
-                                      "--watchdog", str(args.watchdog)] + list(extra))
+                                      "--watchdog", str(args.watchdog), "--reserve-cus", str(args.reserve_cus)]
+                          + list(extra))
 
     phase_log = os.environ.get("HEAT3D_BENCH_PHASES") == "1"
     tp = [time.perf_counter()]

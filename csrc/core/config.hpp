@@ -74,7 +74,7 @@ struct Config {
   bool tile_layers = true;
   bool quiet = false;
   int cpu_threads = 0;
-  int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules
+  int reserve_cus = -1;                   // -1 auto: 8 (one per XCD) for overlapped multi-rank schedules, 0 under long x-slab interiors
 
   // --- schedule / runtime knobs (until round 2 HEAT3D_* environment variables)
   int lag = -1;                   // lagged convergence check of overlapped sweeps (third buffer): -1 auto, 0 off, 1 on

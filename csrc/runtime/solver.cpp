@@ -87,6 +87,11 @@ KernelSpec KernelSpec::parse(const std::string& s) {
   return k;
 }
 
+// interior points of an x-slab share above which the overlapped schedule
+// runs on every CU (no comm reservation; Solver::Solver): the 2-GPU 1024^3
+// share has 5.3e8, the 4-GPU one 2.6e8
+constexpr int64_t kLongSlabInterior = 400000000;
+
 KernelSpec KernelSpec::resolved(DType t) const {
   KernelSpec r = *this;
   const bool f64 = t == DType::F64;
@@ -267,7 +272,22 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   // behind the interior sweep, which holds every CU (LDS / VGPR file full)
   {
     int n = cfg_.reserve_cus;
-    if (n < 0) n = multi_stream() && !comm_->all_local() && comm_->size() > 1 ? 8 : 0;
+    if (n < 0) {
+      n = multi_stream() && !comm_->all_local() && comm_->size() > 1 ? 8 : 0;
+      // ...except under a long x-slab interior, which hides the halo chain
+      // even when the comm kernels wait for a CU: RCCL's kernel (256 threads,
+      // 140 VGPRs, 20 KB LDS; gpurun_out/r7t) cannot sit beside an interior
+      // workgroup (16 waves x 112 VGPRs), so without the reservation it
+      // starts at the next piece boundary, <= ~0.2 ms into the 2-GPU 1024^3
+      // share's ~1.8 ms sweep.  That share (508 x 1022^2 interior points)
+      // ran 4.8-7 % faster on all 256 CUs (proxy: 0.666-0.694 against
+      // 0.715-0.736 ms/step, gpurun_out/r7s, r7u, r7v; 2 reserved CUs were
+      // slower than 8).  The 4-GPU share's whole-x pieces (~0.5 ms) could
+      // hold RCCL's kernel as long as the chain itself, so it keeps them.
+      int64_t least = INT64_MAX;
+      for (const auto& sd : dec_.subs) least = std::min(least, (sd.n[0] - 2 * K_) * sd.n[1] * sd.n[2]);
+      if (n > 0 && tb_ && !block && least >= kLongSlabInterior) n = 0;
+    }
     if (be_->is_gpu() && n > 0) be_->reserve_cus(n);
   }
   preflight_memory();
