@@ -100,6 +100,9 @@ struct PhantomOptions {
   // workgroups per transfer for the wire time (RCCL-like: a few channels
   // stream the face across the link; no burst copy after the wire time)
   bool paced = false;
+  // the delay / copy kernels in RCCL's device-kernel footprint (256 threads,
+  // 140 VGPRs, 20 KB LDS), so that they wait for CUs as RCCL's kernel does
+  bool rccl_footprint = true;
 };
 std::unique_ptr<Comm> make_phantom_comm(int rank, int size, const PhantomOptions& o = {});
 

@@ -28,7 +28,8 @@ class PhantomComm final : public Comm {
  public:
   PhantomComm(int rank, int size, const PhantomOptions& o)
       : rank_(rank), size_(size), gbps_(o.gbps), ar_us_(o.allreduce_us), channels_(o.channels),
-        ar_channels_(o.allreduce_channels), overlap_(o.overlap_copies), paced_(o.paced) {
+        ar_channels_(o.allreduce_channels), overlap_(o.overlap_copies), paced_(o.paced),
+        fat_(o.rccl_footprint) {
     HEAT3D_CHECK(rank >= 0 && rank < size, "phantom rank " << rank << " of " << size);
   }
   ~PhantomComm() override {
@@ -42,6 +43,7 @@ class PhantomComm final : public Comm {
   bool ordered_collectives() const override { return true; }
 
   void exchange(const std::vector<Transfer>& xs, Backend& be, StreamId s) override {
+    be.set_comm_footprint(fat_);
     std::map<int, std::size_t> per_peer;
     for (const auto& x : xs)
       if (x.dst_rank == rank_ && x.src_rank != rank_) per_peer[x.src_rank] += x.bytes;
@@ -53,10 +55,11 @@ class PhantomComm final : public Comm {
     if (paced_ && wire > 0) {
       // every transfer from peer p ends bytes(p) / gbps after it starts
       // workgroups per transfer: the channels, and enough that none must
-      // stream more than ~2 GB/s (at 4 GB/s per 256-lane group, four 16-byte
-      // loads in flight per lane, the 64 GB/s wire ran 9-17 % long beside
-      // the interior sweep: gpurun_out/r7m/proxytrace11)
-      const int per = std::max(channels_, (int)std::ceil(gbps_ / 2.0));
+      // stream more than ~8 GB/s (a 256-lane group with eight 16-byte loads in
+      // flight per lane; at four loads and 4 GB/s per group the 64 GB/s wire
+      // ran 9-17 % long beside the interior sweep, gpurun_out/r7m) — 8 per
+      // 64 GB/s peer, as RCCL's 8 P2P channels (NCCL_MAX_P2P_NCHANNELS)
+      const int per = std::max(channels_, (int)std::ceil(gbps_ / 8.0));
       std::vector<hip::PacedCopy> pc;
       for (const auto& x : xs) {
         if (x.dst_rank != rank_ || x.src_rank == rank_) continue;
@@ -95,6 +98,7 @@ class PhantomComm final : public Comm {
     if (overlap_ && wire > 0) be.delay_since(stamp, wire, s, blocks);
   }
   void allreduce(void*, std::size_t, RedType, RedOp, Backend& be, StreamId s) override {
+    be.set_comm_footprint(fat_);
     if (ar_us_ > 0) be.delay(ar_us_, s, ar_channels_);
   }
   void send(const void*, std::size_t, int, Backend&, StreamId) override {}
@@ -105,7 +109,7 @@ class PhantomComm final : public Comm {
   int rank_, size_;
   double gbps_, ar_us_;
   int channels_, ar_channels_;
-  bool overlap_, paced_;
+  bool overlap_, paced_, fat_;
   Backend* be_ = nullptr;  // owner of slot_ (outlives the communicator, ~Solver)
   void* slot_ = nullptr;   // device clock stamps of the exchanges in flight, one per stream
 };

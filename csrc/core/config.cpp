@@ -137,6 +137,8 @@ std::string Config::usage() {
      << "                            phantom-rank proxy (tools/rank_proxy.py) link emulation\n"
      << "  --phantom-wire serial|overlap|paced  phantom exchange: wire time then copies, copies inside it,\n"
      << "                            or copies paced at the wire rate over the wire time\n"
+     << "  --phantom-footprint rccl|small  phantom comm kernels in RCCL's kernel footprint (256 threads,\n"
+     << "                            140 VGPRs, 20 KB LDS; default) or small (64 threads)\n"
      << "  --quiet                   suppress the banner\n";
   return os.str();
 }
@@ -284,6 +286,11 @@ Config Config::parse(int argc, const char* const* argv) {
       if (v != "serial" && v != "overlap" && v != "paced") throw UsageError("--phantom-wire serial|overlap|paced");
       c.phantom_overlap = v == "overlap";
       c.phantom_paced = v == "paced";
+    }
+    else if (key == "--phantom-footprint") {
+      const std::string v = get("--phantom-footprint");
+      if (v != "rccl" && v != "small") throw UsageError("--phantom-footprint rccl|small");
+      c.phantom_rccl_footprint = v == "rccl";
     }
     else if (key == "--phantom-allreduce-us")
       c.phantom_allreduce_us = to_f64(get("--phantom-allreduce-us"), "--phantom-allreduce-us");

@@ -132,9 +132,10 @@ void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* d
 void check_convergence(DeviceState* s, int slot, void* stream, int count = 1);
 // kernel of `blocks` one-wave workgroups spinning for `us` microseconds on the
 // 100 MHz real-time clock (each holds a wave slot of one CU while it spins)
-void delay(double us, void* stream, int blocks = 1);
+// fat: in RCCL's device-kernel footprint (256 threads, 140 VGPRs, 20 KB LDS)
+void delay(double us, void* stream, int blocks = 1, bool fat = false);
 void stamp(void* slot, void* stream);
-void delay_since(const void* slot, double us, void* stream, int blocks = 1);
+void delay_since(const void* slot, double us, void* stream, int blocks = 1, bool fat = false);
 // a phantom transfer paced at the wire rate (phantom_comm.cpp, --phantom-wire
 // paced): 16-byte aligned, ticks of the 100 MHz clock per 16 bytes of one
 // workgroup's share
@@ -145,7 +146,7 @@ struct PacedCopy {
   double ticks_per16 = 0.0;
 };
 constexpr int kPacedMax = 8;  // transfers per launch
-void paced_copy(const PacedCopy* xs, int n, int per, void* stream);
+void paced_copy(const PacedCopy* xs, int n, int per, void* stream, bool fat = false);
 // placement probe: out[b] = XCC << 8 | SE/SH/CU id of workgroup b (blocks x 64 threads)
 void cu_probe(unsigned* out, int blocks, double us, void* stream);
 // Device-side stream dependencies of per-stream hipGraphs (hip_backend.cpp):

@@ -115,6 +115,9 @@ class Backend {
   // diagnostic: occupy stream s for `us` microseconds with `blocks` spinning
   // workgroups (emulated collective latency / transfer time); no-op on the CPU
   virtual void delay(double /*us*/, StreamId /*s*/, int /*blocks*/ = 1) {}
+  // the phantom transport's delay / copy kernels in RCCL's device-kernel
+  // footprint (GPU backends)
+  virtual void set_comm_footprint(bool /*rccl_like*/) {}
   // device clock stamp into *slot (8 bytes of device memory), and a delay
   // that ends `us` after the stamp (emulated transfers overlapping copies)
   virtual void stamp(void* /*slot*/, StreamId /*s*/) {}

@@ -420,14 +420,17 @@ class HipBackend final : public Backend {
                 const Layout& Ld, const Box& bd, StreamId s) override {
     op(s, [&](hipStream_t st) { hip::copy_box(t, src, Ls, bs, dst, Ld, bd, st); });
   }
-  void delay(double us, StreamId s, int blocks) override { op(s, [&](hipStream_t st) { hip::delay(us, st, blocks); }); }
+  void delay(double us, StreamId s, int blocks) override {
+    op(s, [&](hipStream_t st) { hip::delay(us, st, blocks, fat_comm_); });
+  }
+  void set_comm_footprint(bool rccl_like) override { fat_comm_ = rccl_like; }
   void stamp(void* slot, StreamId s) override { op(s, [&](hipStream_t st) { hip::stamp(slot, st); }); }
   void paced_copy(const std::vector<hip::PacedCopy>& xs, int per, StreamId s) override {
     if (xs.empty()) return;
-    op(s, [&](hipStream_t st) { hip::paced_copy(xs.data(), (int)xs.size(), per, st); });
+    op(s, [&](hipStream_t st) { hip::paced_copy(xs.data(), (int)xs.size(), per, st, fat_comm_); });
   }
   void delay_since(const void* slot, double us, StreamId s, int blocks) override {
-    op(s, [&](hipStream_t st) { hip::delay_since(slot, us, st, blocks); });
+    op(s, [&](hipStream_t st) { hip::delay_since(slot, us, st, blocks, fat_comm_); });
   }
   void check_convergence(DeviceState* st, int slot, StreamId s, int count) override {
     op(s, [&](hipStream_t q) { hip::check_convergence(st, slot, q, count); });
@@ -524,6 +527,7 @@ class HipBackend final : public Backend {
   int dev_;
   int prio_[kNumStreams] = {0, 0, 0};
   int reserved_ = 0;
+  bool fat_comm_ = false;  // phantom delay / copy kernels in RCCL's footprint
   hipStream_t streams_[kNumStreams] = {nullptr, nullptr, nullptr};
   // graph recording state
   bool recording_ = false, in_op_ = false;

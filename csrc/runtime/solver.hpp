@@ -406,6 +406,7 @@ inline PhantomOptions phantom_options(const Config& c) {
   o.channels = c.phantom_channels;
   o.overlap_copies = c.phantom_overlap;
   o.paced = c.phantom_paced;
+  o.rccl_footprint = c.phantom_rccl_footprint;
   o.allreduce_channels = c.phantom_allreduce_channels;
   return o;
 }

@@ -40,6 +40,9 @@ def main() -> int:
                          "copies run inside the wire time (a transport moving data while on the wire); paced: "
                          "the copies move the data at the wire rate over the wire time (RCCL-like channels, "
                          "no burst)")
+    ap.add_argument("--footprint", default="rccl", choices=["rccl", "small"],
+                    help="stand-in comm kernels sized as RCCL's device kernel (256 threads, 140 VGPRs, 20 KB "
+                         "LDS: they wait for CUs as RCCL does) or small (64 threads, round 4's proxy)")
     ap.add_argument("--backend", default="hip")
     ap.add_argument("--extra", default="", help="extra solver flags, e.g. '--no-overlap'")
     ap.add_argument("--preheat-ms", type=float, default=0.0,
@@ -70,7 +73,7 @@ def main() -> int:
     s = HeatSolver(N, iter_max=1 << 40, eps=0.0, dtype=args.dtype, backend=args.backend, decomp=dims,
                    device=0 if args.backend == "hip" else None, phantom=(r, P),
                    extra_args=["--phantom-gbps", str(args.gbps), "--phantom-allreduce-us", str(args.ar_us),
-                               "--phantom-wire", args.wire]
+                               "--phantom-wire", args.wire, "--phantom-footprint", args.footprint]
                    + (args.extra.split() if args.extra else []))
     if args.trace_schedule:
         os.environ["HEAT3D_TRACE"] = "1"
@@ -98,7 +101,7 @@ def main() -> int:
     # the schedule's phases per sweep (after the timed window, as bench.py's 'phases')
     phases = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in s.native.profile_sweeps(8).items()}
     out = {"proxy": "phantom rank", "rank": r, "ranks": P, "dims": list(dims), "grid": args.grid,
-           "dtype": args.dtype, "gbps": args.gbps, "wire": args.wire, "ar_us": args.ar_us, "extra": args.extra,
+           "dtype": args.dtype, "gbps": args.gbps, "wire": args.wire, "footprint": args.footprint, "ar_us": args.ar_us, "extra": args.extra,
            "steps": args.steps, "warmup": args.warmup, "preheat_sweeps": preheat,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "kernel": s.kernel,
            "reserved_cus": s.native.reserved_cus, "graph_launches": s.native.graph_launches,
