@@ -102,7 +102,8 @@ struct PhantomOptions {
   bool paced = false;
   // the delay / copy kernels in RCCL's device-kernel footprint (256 threads,
   // 140 VGPRs, 20 KB LDS), so that they wait for CUs as RCCL's kernel does
-  bool rccl_footprint = true;
+  // (opt-in: the proxy numbers of rounds 2-5 use the small kernels)
+  bool rccl_footprint = false;
 };
 std::unique_ptr<Comm> make_phantom_comm(int rank, int size, const PhantomOptions& o = {});
 

@@ -55,11 +55,11 @@ class PhantomComm final : public Comm {
     if (paced_ && wire > 0) {
       // every transfer from peer p ends bytes(p) / gbps after it starts
       // workgroups per transfer: the channels, and enough that none must
-      // stream more than ~8 GB/s (a 256-lane group with eight 16-byte loads in
-      // flight per lane; at four loads and 4 GB/s per group the 64 GB/s wire
-      // ran 9-17 % long beside the interior sweep, gpurun_out/r7m) — 8 per
-      // 64 GB/s peer, as RCCL's 8 P2P channels (NCCL_MAX_P2P_NCHANNELS)
-      const int per = std::max(channels_, (int)std::ceil(gbps_ / 8.0));
+      // stream more than ~2 GB/s: a 256-lane group moves ~4 GB/s beside the
+      // interior sweep whether it keeps four or eight 16-byte loads in flight
+      // per lane (8 groups per 64 GB/s transfer ran the wire 2x long,
+      // gpurun_out/r7x; 16 ran it 9-17 % long, r7m)
+      const int per = std::max(channels_, (int)std::ceil(gbps_ / 2.0));
       std::vector<hip::PacedCopy> pc;
       for (const auto& x : xs) {
         if (x.dst_rank != rank_ || x.src_rank == rank_) continue;

@@ -138,7 +138,7 @@ std::string Config::usage() {
      << "  --phantom-wire serial|overlap|paced  phantom exchange: wire time then copies, copies inside it,\n"
      << "                            or copies paced at the wire rate over the wire time\n"
      << "  --phantom-footprint rccl|small  phantom comm kernels in RCCL's kernel footprint (256 threads,\n"
-     << "                            140 VGPRs, 20 KB LDS; default) or small (64 threads)\n"
+     << "                            140 VGPRs, 20 KB LDS) or small (64 threads; default)\n"
      << "  --quiet                   suppress the banner\n";
   return os.str();
 }

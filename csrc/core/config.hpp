@@ -103,7 +103,7 @@ struct Config {
   int phantom_allreduce_channels = 2;
   bool phantom_overlap = false;   // --phantom-wire overlap: copies inside the emulated wire time
   bool phantom_paced = false;
-  bool phantom_rccl_footprint = true;  // --phantom-footprint rccl|small: stand-in kernels sized as RCCL's     // --phantom-wire paced: copies paced at the wire rate for the wire time
+  bool phantom_rccl_footprint = false;  // --phantom-footprint rccl|small: stand-in kernels sized as RCCL's     // --phantom-wire paced: copies paced at the wire rate for the wire time
 
   // Parse argv.  Throws UsageError on a malformed command line.
   static Config parse(int argc, const char* const* argv);

@@ -40,7 +40,7 @@ def main() -> int:
                          "copies run inside the wire time (a transport moving data while on the wire); paced: "
                          "the copies move the data at the wire rate over the wire time (RCCL-like channels, "
                          "no burst)")
-    ap.add_argument("--footprint", default="rccl", choices=["rccl", "small"],
+    ap.add_argument("--footprint", default="small", choices=["rccl", "small"],
                     help="stand-in comm kernels sized as RCCL's device kernel (256 threads, 140 VGPRs, 20 KB "
                          "LDS: they wait for CUs as RCCL does) or small (64 threads, round 4's proxy)")
     ap.add_argument("--backend", default="hip")
