@@ -267,6 +267,13 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
   fake_allreduce_us_ = cfg_.fake_allreduce_us;
   be_->set_graph_wait_timeout(cfg_.watchdog_s);
   chain_ = comm_->ordered_collectives() && !comm_->all_local() && comm_->size() > 1;
+  // a long x-slab interior (the 2-GPU 1024^3 share): the halo chain hides
+  // under it with room to spare (no CU reservation)
+  {
+    int64_t least = INT64_MAX;
+    for (const auto& sd : dec_.subs) least = std::min(least, (sd.n[0] - 2 * K_) * sd.n[1] * sd.n[2]);
+    long_slab_ = tb_overlap_ && !block && least >= kLongSlabInterior && !comm_->all_local() && comm_->size() > 1;
+  }
   // CU reservation for the overlapped schedule of a real multi-rank job
   // (RCCL or its phantom): the comm / boundary / check kernels must not queue
   // behind the interior sweep, which holds every CU (LDS / VGPR file full)
@@ -284,9 +291,7 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
       // 0.715-0.736 ms/step, gpurun_out/r7s, r7u, r7v; 2 reserved CUs were
       // slower than 8).  The 4-GPU share's whole-x pieces (~0.5 ms) could
       // hold RCCL's kernel as long as the chain itself, so it keeps them.
-      int64_t least = INT64_MAX;
-      for (const auto& sd : dec_.subs) least = std::min(least, (sd.n[0] - 2 * K_) * sd.n[1] * sd.n[2]);
-      if (n > 0 && tb_ && !block && least >= kLongSlabInterior) n = 0;
+      if (n > 0 && long_slab_) n = 0;
     }
     if (be_->is_gpu() && n > 0) be_->reserve_cus(n);
   }
@@ -661,7 +666,9 @@ KernelSpec Solver::spec_for_depth(int Kp) const {
 // kernel-level timing of round 5's first boxes had the pair form 1.5% slower
 // (profiles/fp64_pairs_r05.md).  Only where the sweeps run alone as timed;
 // under the overlapped multi-rank schedule the standalone timing picked the
-// pairs and they ran no faster there.
+// pairs and they ran no faster there; on the 2-GPU share, whose interior
+// hides its halo chain, the pair form timed 1 % faster and ran the same
+// (0.6775-0.6793 against 0.6776-0.6804 ms/step, gpurun_out/r7y).
 bool Solver::pick_sweep_form() const {
   if (!tb_ || !be_->is_gpu() || dt_ != DType::F64 || has_halo_ || local_.size() != 1 || cfg_.kernel2 != "auto" ||
       kspec2_.kind != KernelSpec::TBL)

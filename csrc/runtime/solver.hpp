@@ -289,7 +289,8 @@ class Solver {
   std::vector<Local> local_;
   bool has_halo_ = false;  // any face with a neighbour on any local subdomain
   bool overlap_ = true;
-  bool tb_overlap_ = false;   // sweeps: interior || (deep halo -> boundary slabs)
+  bool tb_overlap_ = false;
+  bool long_slab_ = false;    // x-slab share whose interior hides the halo chain (no CU reservation)   // sweeps: interior || (deep halo -> boundary slabs)
   int64_t hd_[3] = {1, 1, 1}; // ghost depth per axis (K on split axes with temporal blocking, K+1 with long_halo_)
   int64_t xd_[3] = {1, 1, 1}; // regular exchange depth per axis (K on split axes with temporal blocking)
   // Long sweeps (depth K+1) across halos: ghosts allocated K+1 deep on split

@@ -195,6 +195,15 @@ def test_sweep_pair_deep_halo_matches_cpu(h3d, gpu, kernel, n0, box_x, side):
     _deep_halo_case(h3d, gpu, kernel, torch.float32, n0, box_x, side)
 
 
+@pytest.mark.parametrize("kernel", PAIR_F64[2] + PAIR_F64[3] + PAIR_F64[4])
+@pytest.mark.parametrize("n0,box_x,side", [(4, (0, 4), "both"), (9, (0, 9), "hi"), (12, (4, 8), "both"),
+                                            (30, (0, 30), "both"), (40, (3, 37), "both")])
+def test_sweep_pair_f64_deep_halo_matches_cpu(h3d, gpu, kernel, n0, box_x, side):
+    """The fp64 16-byte pair kernel on the slab path (the interior of a long
+    x-slab share takes it when the start-up timing finds it faster)."""
+    _deep_halo_case(h3d, gpu, kernel, torch.float64, n0, box_x, side)
+
+
 @pytest.mark.parametrize("kernel", ["tl3", "tl3:1:3:1:16:0:3"])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("n0,box_x,side,ny", [(12, (0, 3), "both", 64), (12, (9, 12), "both", 64),
