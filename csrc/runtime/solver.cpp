@@ -89,8 +89,8 @@ KernelSpec KernelSpec::parse(const std::string& s) {
 
 // interior points of an x-slab share above which the overlapped schedule
 // runs on every CU (no comm reservation; Solver::Solver): the 2-GPU 1024^3
-// share has 5.3e8, the 4-GPU one 2.6e8
-constexpr int64_t kLongSlabInterior = 400000000;
+// share has 5.3e8, the 4-GPU one 2.6e8, the 8-GPU one 1.3e8
+constexpr int64_t kLongSlabInterior = 200000000;
 
 KernelSpec KernelSpec::resolved(DType t) const {
   KernelSpec r = *this;
@@ -289,8 +289,10 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
       // share's ~1.8 ms sweep.  That share (508 x 1022^2 interior points)
       // ran 4.8-7 % faster on all 256 CUs (proxy: 0.666-0.694 against
       // 0.715-0.736 ms/step, gpurun_out/r7s, r7u, r7v; 2 reserved CUs were
-      // slower than 8).  The 4-GPU share's whole-x pieces (~0.5 ms) could
-      // hold RCCL's kernel as long as the chain itself, so it keeps them.
+      // slower than 8), the 4-GPU share (250 planes) 1.3-11 % (0.385-0.415
+      // against 0.421-0.435; the low end with the stand-in comm kernels in
+      // RCCL's footprint, which wait for a CU as RCCL's does: r7t, r7w).  The
+      // 8-GPU share keeps the reservation (-1.4 to +5 %, r7t, r7w).
       if (n > 0 && long_slab_) n = 0;
     }
     if (be_->is_gpu() && n > 0) be_->reserve_cus(n);
