@@ -204,6 +204,15 @@ def run_rank(args) -> int:
         return 2
     dev = info.local_rank % ndev
     torch.cuda.set_device(dev)
+    # Ranks per GPU (rehearsals put a whole node's ranks on one device): the
+    # overlapped schedule's per-stream graphs wait across streams with
+    # spinning device-side kernels, which assume the process's hardware queues
+    # stay resident.  Eight processes on one GPU oversubscribe its queues and
+    # the 8-rank rehearsal hung in its warm-up (gpurun_out/r8f), eager it ran
+    # (r8g); 2-4 processes on one GPU run the graphs (tests/test_gpu_rccl.py).
+    # So more than 4 ranks per device replay eagerly; one per GPU never does.
+    per_dev = -(-int(os.environ.get("LOCAL_WORLD_SIZE", world)) // ndev)
+    stream_graphs = per_dev <= 4
 
     G = args.grid
     N = (G, G, G)
@@ -239,7 +248,8 @@ def run_rank(args) -> int:
                           decomp=dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
                           device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
-                          extra_args=["--temporal", str(args.temporal), "--kernel2", args.kernel2,
+                          extra_args=([] if stream_graphs else ["--no-stream-graphs"]) +
+                                     ["--temporal", str(args.temporal), "--kernel2", args.kernel2,
                                       "--watchdog", str(args.watchdog), "--reserve-cus", str(args.reserve_cus)]
                           + list(extra))
 
@@ -367,6 +377,7 @@ def run_rank(args) -> int:
                    + (f" ({args.virtual_ranks} virtual ranks on 1 GPU)" if args.virtual_ranks > 1 else ""),
                    "kernel": kernel, "temporal_K": K, "field_buffers": nbuf,
                    "graph_requested": not args.no_graph, "graph_used": graph_launches > 0,
+                   "stream_graphs": stream_graphs, "ranks_per_device": per_dev,
                    "graph_launches": graph_launches,
                    "overlap": not args.no_overlap, "comm": comm_name, "reserved_cus": reserved,
                    "preheat_sweeps": preheat},
