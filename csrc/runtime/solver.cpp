@@ -291,8 +291,10 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
       // 0.715-0.736 ms/step, gpurun_out/r7s, r7u, r7v; 2 reserved CUs were
       // slower than 8), the 4-GPU share (250 planes) 1.3-11 % (0.385-0.415
       // against 0.421-0.435; the low end with the stand-in comm kernels in
-      // RCCL's footprint, which wait for a CU as RCCL's does: r7t, r7w).  The
-      // 8-GPU share keeps the reservation (-1.4 to +5 %, r7t, r7w).
+      // RCCL's footprint, which wait for a CU as RCCL's does: r7t, r7w; at
+      // 40 GB/s links 4-6 %, r8k).  The 8-GPU share keeps the reservation: its
+      // chain runs as long as its interior, so an RCCL kernel that waits for a
+      // CU would show, and the proxy models disagree (+1.2 % to -8.6 %, r8l).
       if (n > 0 && long_slab_) n = 0;
     }
     if (be_->is_gpu() && n > 0) be_->reserve_cus(n);
