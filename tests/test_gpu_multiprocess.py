@@ -71,6 +71,22 @@ def test_phantom_rank_gpu(h3d, gpu, rank, size, decomp, wire):
     assert st["iter"] == 40 and st["done"] == 0, st
 
 
+@pytest.mark.parametrize("n,rank,size,decomp,reserved", [(800, 0, 2, (2, 1, 1), 0), (800, 1, 8, (8, 1, 1), 8),
+                                                          (400, 1, 2, (2, 1, 1), 8), (800, 7, 8, (2, 2, 2), 8)])
+def test_comm_cu_reservation_rule(h3d, gpu, n, rank, size, decomp, reserved):
+    """The overlapped multi-rank schedule keeps 8 CUs for the comm kernels,
+    except under x-slab interiors of >= 2e8 points (394 x 798^2 here; the 2-
+    and 4-GPU shares of 1024^3), which hide the halo chain even when RCCL's
+    kernel waits for a CU (Solver::Solver, profiles/r05/proxy_runs.md)."""
+    s = h3d.HeatSolver((n,) * 3, 1 << 40, 0.0, backend="hip", device=0, decomp=decomp, phantom=(rank, size),
+                       extra_args=["--temporal", "3", "--phantom-gbps", "64"])
+    assert s.native.reserved_cus == reserved, (n, decomp, s.native.reserved_cus)
+    s.initialize()
+    s.step(6)
+    s.synchronize()
+    assert s.state()["iter"] == 6
+
+
 @pytest.mark.parametrize("rank,size,decomp", [(1, 8, (8, 1, 1)), (5, 8, (2, 2, 2))])
 def test_phantom_paced_wire_moves_the_same_data(h3d, gpu, rank, size, decomp):
     """--phantom-wire paced (copies paced at the wire rate by a few workgroups
