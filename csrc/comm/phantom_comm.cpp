@@ -16,6 +16,7 @@
 // (tools/rank_proxy.py).
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <map>
 
 #include "comm.hpp"
@@ -52,7 +53,12 @@ class PhantomComm final : public Comm {
     // bytes / (GB/s) in us, every peer's channels in flight at once
     const double wire = worst && gbps_ > 0 ? worst / (gbps_ * 1e3) : 0.0;
     const int blocks = channels_ * (int)per_peer.size();
-    if (paced_ && wire > 0) {
+    // the paced copy moves 16-byte words: other transfers take the serial wire
+    bool aligned16 = true;
+    for (const auto& x : xs)
+      aligned16 &= x.bytes % 16 == 0 && reinterpret_cast<std::uintptr_t>(x.src) % 16 == 0 &&
+                   reinterpret_cast<std::uintptr_t>(x.dst) % 16 == 0;
+    if (paced_ && wire > 0 && aligned16) {
       // every transfer from peer p ends bytes(p) / gbps after it starts
       // workgroups per transfer: the channels, and enough that none must
       // stream more than ~2 GB/s: a 256-lane group moves ~4 GB/s beside the

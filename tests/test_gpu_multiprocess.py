@@ -71,6 +71,18 @@ def test_phantom_rank_gpu(h3d, gpu, rank, size, decomp, wire):
     assert st["iter"] == 40 and st["done"] == 0, st
 
 
+def test_phantom_paced_wire_odd_fp32_faces(h3d, gpu):
+    """--phantom-wire paced with fp32 faces that are not whole 16-byte words
+    (2x2x2 blocks of a 91^3 grid): those exchanges take the serial wire."""
+    s = h3d.HeatSolver((91, 91, 91), 1 << 40, 0.0, dtype="fp32", backend="hip", device=0, decomp=(2, 2, 2),
+                       phantom=(5, 8), extra_args=["--temporal", "3", "--phantom-gbps", "50",
+                                                   "--phantom-wire", "paced"])
+    s.initialize()
+    s.step(12)
+    s.synchronize()
+    assert s.state()["iter"] == 12
+
+
 @pytest.mark.parametrize("n,rank,size,decomp,reserved", [(800, 0, 2, (2, 1, 1), 0), (800, 1, 8, (8, 1, 1), 8),
                                                           (400, 1, 2, (2, 1, 1), 8), (800, 7, 8, (2, 2, 2), 8)])
 def test_comm_cu_reservation_rule(h3d, gpu, n, rank, size, decomp, reserved):
