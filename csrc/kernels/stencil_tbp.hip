@@ -474,6 +474,12 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
     ga.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
     const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
     HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl pair: bad block count " << nblocks);
+    if (trace_enabled())
+      std::fprintf(stderr,
+                   "[heat3d trace] tl pair K=%d box x %lld: zs=%d L=%d seg=%d tiles=%dx%d blocks=%lld slots=%d "
+                   "(model %.1f)\n",
+                   K, (long long)nxb, zs, Lx, xp.seg, ga.nzb, ga.nyb, (long long)nblocks, slots,
+                   xplan_makespan(xp, nxb, tiles, slots, 2 * (K - 1), U));
     hipLaunchKernelGGL((stencil_tbp<T, R, WY, K, Q, AUX>), dim3((unsigned)nblocks), dim3(64 * WY), 0, s,
                        static_cast<const T*>(p.in), static_cast<T*>(p.out), ga, (T)p.D[0], (T)p.D[1], (T)p.D[2], r,
                        done);
