@@ -5,6 +5,8 @@
 # summary is one 1024^3 sweep (tools/summarize_rocprof.py takes the median).
 # Usage: tools/pmc_passes.sh OUTDIR VARIANT [N] [DTYPE] [SET]
 #   SET = default (issue, LDS, L2 / HBM bytes) | latency (L1 / TLB stalls, L2 read latency, TA / TD)
+#   PMC_SHAPE="X Y Z": sweep that owned box instead of (N-2)^3 (tune.py --shape), e.g. "3 1022 1022"
+#   for the 8-GPU share's boundary slab
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -30,7 +32,8 @@ fi
 i=0
 for p in "${passes[@]}"; do
   timeout -s KILL 90 rocprofv3 --pmc $p -d "$out/p$i" -o run --output-format csv -- \
-    python3 "$ROOT/tools/tune.py" --n "$n" --dtype "$dt" --variants "$var" --iters 4 --rounds 1 > "$out/p$i.log" 2>&1
+    python3 "$ROOT/tools/tune.py" --n "$n" --dtype "$dt" --variants "$var" --iters 4 --rounds 1 \
+    ${PMC_SHAPE:+--shape $PMC_SHAPE} > "$out/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   [ $rc -ne 0 ] && exit $rc
