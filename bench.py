@@ -21,9 +21,13 @@ Launch (the reference: ``mpirun -n P ./heat3D ...``, heat3D.cu:203-205):
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
       one rank per process as launched (RANK / WORLD_SIZE from torchrun).
 
-torch.distributed (gloo) is used only to bootstrap: the ncclUniqueId
-broadcast, host barriers and the max-over-ranks of the timed interval.  All
-per-iteration traffic goes through the native RCCL communicator.
+The ranks never import torch: one HIP runtime per process, /opt/rocm's HIP 7.2
+and RCCL 2.27 (the native CLI's), not the HIP 7.0 / RCCL 2.26 copies PyTorch
+bundles under the same sonames (HEAT3D_RUNTIME=rocm, _native.py; the JSON's
+"runtime" block records the versions and library files each rank bound).
+The host bootstrap is native too (HostGroup: the ncclUniqueId broadcast, host
+barriers, the max-over-ranks of the timed interval).  All per-iteration
+traffic goes through the native RCCL communicator.
 """
 from __future__ import annotations
 
@@ -122,12 +126,13 @@ def _free_port() -> int:
 def launch(args, argv) -> int:
     n = args.gpus
     port = _free_port()
+    hg_port = _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   HEAT3D_BENCH_WORKER="1")
+                   HEAT3D_HOSTGROUP_PORT=str(hg_port), HEAT3D_BENCH_WORKER="1")
         if args.rccl_host_split:
             env.update(NCCL_HOSTID=f"heat3d-bench-rank{r}", NCCL_SOCKET_IFNAME="lo")
         # each worker leads its own process group so that the watchdog can end
@@ -176,12 +181,13 @@ def launch(args, argv) -> int:
 # one rank
 
 def run_rank(args) -> int:
-    import torch
-
+    # one HIP runtime per process, /opt/rocm's: never import torch here
+    os.environ.setdefault("HEAT3D_RUNTIME", "rocm")
     import heat3d_amd
     from heat3d_amd import HeatSolver
     from heat3d_amd.parallel import SLAB_MIN_LINK_GBPS, best_dims_for, choose_dims
-    from heat3d_amd.parallel.distributed import all_gather_objects, barrier, init_process_group, max_over_ranks
+    from heat3d_amd.parallel.distributed import (HostGroup, all_gather_objects, barrier, env_info,
+                                                 max_over_ranks)
     from heat3d_amd.utils.metrics import roofline_glups
 
     ext = heat3d_amd.native()
@@ -189,9 +195,11 @@ def run_rank(args) -> int:
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
-    # torch.distributed is the bootstrap only (gloo): the per-iteration halo and
-    # all-reduce traffic goes through the native RCCL communicator
-    info, group = init_process_group("gloo" if world > 1 else None)
+    # host bootstrap (native TCP star, no torch): the ncclUniqueId broadcast,
+    # barriers and the max over ranks; the per-iteration halo and all-reduce
+    # traffic goes through the native RCCL communicator
+    info = env_info()
+    group = HostGroup.from_env(timeout_s=args.timeout) if world > 1 else None
     rank = info.rank
     if args.rccl_host_split and world > 1 and "NCCL_HOSTID" not in os.environ:
         # under an external launcher (torchrun): every rank its own RCCL "host"
@@ -203,7 +211,7 @@ def run_rank(args) -> int:
         print("bench.py: no HIP device visible", file=sys.stderr)
         return 2
     dev = info.local_rank % ndev
-    torch.cuda.set_device(dev)
+    runtime = heat3d_amd.runtime()
     # Ranks per GPU (rehearsals put a whole node's ranks on one device): the
     # overlapped schedule's per-stream graphs wait across streams with
     # spinning device-side kernels, which assume the process's hardware queues
@@ -293,13 +301,13 @@ def run_rank(args) -> int:
                if args.preheat_ms > 0 else 0)
     phase("preheat enqueued")
     barrier(group)
-    torch.cuda.synchronize()
+    ext.device_synchronize(dev)
     phase("barrier")
     t0 = time.perf_counter()
     s.step(args.steps)
     phase("timed steps enqueued")
     s.synchronize()
-    torch.cuda.synchronize()
+    ext.device_synchronize(dev)
     barrier(group)
     t1 = time.perf_counter()
     dt = max_over_ranks(t1 - t0, group)
@@ -321,6 +329,7 @@ def run_rank(args) -> int:
     # remainder policy (Solver::calibrate_remainders): which n mod K end in
     # K+1-step sweeps, from the start-up sweep timings (ms)
     placement = all_gather_objects({"rank": rank, "device": dev, "host": socket.gethostname(),
+                                    "hip_library": runtime["hip_library"], "rccl_library": runtime["rccl_library"],
                                     "link_probe_gbps": None if link is None else round(link, 3),
                                     "dims": list(dims), "rccl_p2p_channels": s.native.rccl_p2p_channels or None,
                                     "subdomain": list(s.native.local_subdomain(0)["n"]), "x_schedules": xs,
@@ -402,6 +411,8 @@ def run_rank(args) -> int:
         "temporal_roofline_glups_per_gpu": round(5.6e12 / (2 * esize / max(1, K)) / 1e9, 1),
         "vs_temporal_roofline": round(value / world / (5.6e12 / (2 * esize / max(1, K)) / 1e9), 4),
         "time_to_converge": ttc,
+        # the HIP runtime / RCCL the ranks ran on (rank 0; every rank's files in placement)
+        "runtime": dict(runtime, torch_loaded="torch" in sys.modules),
         "phases": phases,
         "baseline_note": "reference publishes no numbers (BASELINE.md); single-step roofline = "
                          "6.29 TB/s / (2*esize) per GPU",
@@ -413,10 +424,7 @@ def run_rank(args) -> int:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     if world > 1:
-        import torch.distributed as dist
-
         barrier(group)
-        dist.destroy_process_group()
     return 0
 
 

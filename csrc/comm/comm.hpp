@@ -111,6 +111,7 @@ std::unique_ptr<Comm> make_phantom_comm(int rank, int size, const PhantomOptions
 bool rccl_available();
 std::string rccl_unique_id();
 std::string rccl_version();
+std::string rccl_library_path();  // the librccl.so.1 this process is bound to
 // shared: one communicator for halos and all-reduces (else a second one from
 // ncclCommSplit); graph: its calls may be recorded into hipGraphs.
 struct RcclOptions {

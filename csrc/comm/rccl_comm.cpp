@@ -24,9 +24,11 @@
 // so the chain costs the next halo nothing.  If ncclCommSplit is unavailable
 // both kinds share one communicator: RCCL then serialises them in host issue
 // order, which is the same total order.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
@@ -55,6 +57,18 @@ std::string rccl_version() {
   std::ostringstream os;
   os << v / 10000 << "." << (v / 100) % 100 << "." << v % 100;
   return os.str();
+}
+
+// The file the dynamic linker bound librccl.so.1 to in this process (torch
+// bundles a copy under the same soname; which one a process runs on depends
+// on what it loaded first, so the bench records it).
+std::string rccl_library_path() {
+  Dl_info di;
+  if (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &di) && di.dli_fname) {
+    char buf[4096];
+    return realpath(di.dli_fname, buf) ? std::string(buf) : std::string(di.dli_fname);
+  }
+  return "unknown";
 }
 
 namespace {

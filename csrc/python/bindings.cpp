@@ -215,6 +215,46 @@ PYBIND11_MODULE(_heat3d, m) {
   });
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
+  // the HIP runtime / RCCL this process is bound to (bench JSON "runtime")
+  m.def("runtime_info", []() {
+    const HipRuntimeInfo h = hip_runtime_info();
+    py::dict d;
+    d["hip_runtime_version"] = h.runtime_version;
+    d["hip_driver_version"] = h.driver_version;
+    d["hip_library"] = h.library;
+    d["rccl_version"] = rccl_version();
+    d["rccl_library"] = rccl_library_path();
+    return d;
+  });
+  m.def("device_synchronize", [](int device) {
+    py::gil_scoped_release nogil;
+    hip_device_synchronize(device);
+  });
+  // Host collectives of a job without torch (bench.py's ranks): a star of TCP
+  // connections to rank 0 (net::Bootstrap), kept open for the job.
+  py::class_<net::Bootstrap>(m, "HostGroup")
+      .def(py::init([](int rank, int size, const std::string& master, int port, double timeout_s) {
+             py::gil_scoped_release nogil;
+             return std::unique_ptr<net::Bootstrap>(new net::Bootstrap(rank, size, master, port, timeout_s));
+           }),
+           py::arg("rank"), py::arg("size"), py::arg("master"), py::arg("port"), py::arg("timeout_s") = 600.0)
+      .def("allgather", [](net::Bootstrap& b, py::bytes blob) {
+        std::string s(blob);
+        std::vector<std::string> all;
+        {
+          py::gil_scoped_release nogil;
+          all = b.allgather(s);
+        }
+        py::list out;
+        for (auto& a : all) out.append(py::bytes(a));
+        return out;
+      })
+      .def("barrier", [](net::Bootstrap& b) {
+        py::gil_scoped_release nogil;
+        b.barrier();
+      })
+      .def_property_readonly("rank", &net::Bootstrap::rank)
+      .def_property_readonly("size", &net::Bootstrap::size);
   // Which CUs a stream created with a CU mask reaches: runs the placement
   // probe on hipExtStreamCreateWithCUMask(mask) (an empty mask: a plain
   // stream) and returns the distinct (XCC << 8 | SE/SH/CU) ids seen.

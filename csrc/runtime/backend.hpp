@@ -135,5 +135,16 @@ class Backend {
 std::unique_ptr<Backend> make_cpu_backend(int threads);
 std::unique_ptr<Backend> make_hip_backend(int device);
 int hip_device_count();  // 0 when no GPU / no driver
+// The HIP runtime this process is bound to: hipRuntimeGetVersion (e.g.
+// 70253121 = 7.2.53121) and the file libamdhip64.so.7 resolved to.  PyTorch
+// bundles a HIP 7.0 runtime under the same soname: a process that imports
+// torch before the solver runs on torch's copy (bench.py and smoke() do not).
+struct HipRuntimeInfo {
+  int runtime_version = 0, driver_version = 0;
+  std::string library;
+};
+HipRuntimeInfo hip_runtime_info();
+// block until every stream of `device` is idle (hipDeviceSynchronize)
+void hip_device_synchronize(int device);
 
 }  // namespace heat3d

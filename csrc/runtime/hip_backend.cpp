@@ -61,6 +61,23 @@ int hip_device_count() {
   return n;
 }
 
+HipRuntimeInfo hip_runtime_info() {
+  HipRuntimeInfo r;
+  if (hipRuntimeGetVersion(&r.runtime_version) != hipSuccess) (void)hipGetLastError();
+  if (hipDriverGetVersion(&r.driver_version) != hipSuccess) (void)hipGetLastError();
+  Dl_info di;
+  if (dladdr(reinterpret_cast<void*>(&hipRuntimeGetVersion), &di) && di.dli_fname) {
+    char buf[4096];
+    r.library = realpath(di.dli_fname, buf) ? std::string(buf) : std::string(di.dli_fname);
+  }
+  return r;
+}
+
+void hip_device_synchronize(int device) {
+  HIP_CHECK(hipSetDevice(device));
+  HIP_CHECK(hipDeviceSynchronize());
+}
+
 namespace {
 
 struct Roctx {

@@ -23,10 +23,20 @@ from __future__ import annotations
 
 __version__ = "0.1.0"
 
-from . import _native  # noqa: F401  (imports torch first: one HIP runtime)
+from . import _native  # noqa: F401  (the one HIP runtime of the process: _native.RUNTIME)
 from ._native import available as native_available  # noqa: F401
-from ._native import native  # noqa: F401
-from . import models, ops, parallel, utils  # noqa: F401,E402
+from ._native import native, runtime  # noqa: F401
+from . import models, parallel, utils  # noqa: F401,E402
 from .models.heat3d import HeatEquation3D, HeatSolver  # noqa: F401
 
-__all__ = ["HeatEquation3D", "HeatSolver", "native", "native_available", "__version__"]
+__all__ = ["HeatEquation3D", "HeatSolver", "native", "native_available", "runtime", "__version__"]
+
+
+def __getattr__(name):
+    # ops works on torch tensors: imported on first use, so that a torch-free
+    # process (HEAT3D_RUNTIME=rocm) never loads torch
+    if name == "ops":
+        import importlib
+
+        return importlib.import_module(__name__ + ".ops")
+    raise AttributeError(name)

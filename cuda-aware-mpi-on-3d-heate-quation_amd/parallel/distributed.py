@@ -17,6 +17,7 @@ communicators:
 """
 from __future__ import annotations
 
+import json
 import os
 import socket
 from dataclasses import dataclass, field
@@ -98,8 +99,70 @@ def _route_ip(master: str) -> str:
         return "127.0.0.1"
 
 
+class HostGroup:
+    """Torch-free host collectives of a job (one process per rank).
+
+    A star of TCP connections to rank 0 held open for the job (native
+    ``net::Bootstrap``, the CLI's bootstrap, heat3D.cu:203-205's MPI_Init
+    analogue).  bench.py's ranks use it instead of torch.distributed so that
+    the process never loads torch, whose bundled HIP 7.0 runtime / RCCL 2.26
+    would otherwise be the ones the solver binds to (one runtime per process:
+    /opt/rocm's).  Objects travel as JSON.
+    """
+
+    def __init__(self, rank: int, size: int, master: str = "127.0.0.1", port: Optional[int] = None,
+                 timeout_s: float = 600.0):
+        self.rank, self.size = int(rank), int(size)
+        if port is None:
+            port = host_group_port()
+        self._b = native().HostGroup(self.rank, self.size, master, int(port), float(timeout_s)) if size > 1 else None
+
+    @classmethod
+    def from_env(cls, timeout_s: float = 600.0) -> "HostGroup":
+        info = env_info()
+        return cls(info.rank, info.world_size, info.master_addr, None, timeout_s)
+
+    def allgather(self, obj) -> list:
+        if self._b is None:
+            return [obj]
+        blobs = self._b.allgather(json.dumps(obj).encode())
+        return [json.loads(b.decode()) for b in blobs]
+
+    def allgather_bytes(self, blob: bytes) -> List[bytes]:
+        return [blob] if self._b is None else list(self._b.allgather(blob))
+
+    def barrier(self) -> None:
+        if self._b is not None:
+            self._b.barrier()
+
+    def max(self, value: float) -> float:
+        return max(float(v) for v in self.allgather(float(value)))
+
+
+def host_group_port() -> int:
+    """HEAT3D_HOSTGROUP_PORT, else MASTER_PORT + 2 (torchrun's agent store owns
+    MASTER_PORT, the native CLI bootstrap MASTER_PORT + 1)."""
+    v = os.environ.get("HEAT3D_HOSTGROUP_PORT")
+    if v:
+        return int(v)
+    return int(os.environ.get("MASTER_PORT", "29500")) + 2
+
+
 def native_comm_args(kind: str, group=None) -> NativeCommArgs:
-    """Bootstrap arguments for ``_heat3d.Solver`` in a torch.distributed job."""
+    """Bootstrap arguments for ``_heat3d.Solver``: through a :class:`HostGroup`
+    (torch-free), else through torch.distributed."""
+    if isinstance(group, HostGroup):
+        if group.size == 1:
+            return NativeCommArgs()
+        rank, size = group.rank, group.size
+        if kind == "rccl":
+            uid = group.allgather_bytes(native().rccl_unique_id() if rank == 0 else b"")[0]
+            return NativeCommArgs(rank, size, "rccl", unique_id=uid)
+        if kind in ("socket", "staged"):
+            fd, port = native().socket_listen()
+            me = f"{_route_ip(os.environ.get('MASTER_ADDR', '127.0.0.1'))}:{port}"
+            return NativeCommArgs(rank, size, kind, listen_fd=fd, addrs=[str(a) for a in group.allgather(me)])
+        raise ValueError(f"unknown native comm kind {kind!r}")
     import torch.distributed as dist
 
     if not dist.is_initialized() or dist.get_world_size() == 1:
@@ -119,6 +182,9 @@ def native_comm_args(kind: str, group=None) -> NativeCommArgs:
 
 
 def barrier(group=None):
+    if isinstance(group, HostGroup):
+        group.barrier()
+        return
     import torch.distributed as dist
 
     if dist.is_initialized():
@@ -126,7 +192,10 @@ def barrier(group=None):
 
 
 def all_gather_objects(obj, group=None) -> list:
-    """Host-side all-gather of a picklable object (bootstrap group); [obj] alone."""
+    """Host-side all-gather of an object (HostGroup: JSON; torch gloo group:
+    pickle); [obj] alone."""
+    if isinstance(group, HostGroup):
+        return group.allgather(obj)
     import torch.distributed as dist
 
     if not dist.is_initialized() or dist.get_world_size() == 1:
@@ -137,7 +206,9 @@ def all_gather_objects(obj, group=None) -> list:
 
 
 def max_over_ranks(value: float, group=None) -> float:
-    """Host-side max of a scalar over ranks (gloo bootstrap group)."""
+    """Host-side max of a scalar over ranks (HostGroup or gloo bootstrap group)."""
+    if isinstance(group, HostGroup):
+        return group.max(value)
     import torch
     import torch.distributed as dist
 
