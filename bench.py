@@ -68,6 +68,12 @@ def parse_args(argv=None):
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--stream-graphs", default="auto", choices=["auto", "on", "off"],
+                    help="the overlapped multi-rank schedule as per-stream hipGraphs (auto: unless more than 4 "
+                         "ranks share a GPU); a start-up canary with a short device-wait timeout falls back to "
+                         "eager replay in-process when they do not hold")
+    ap.add_argument("--graph-canary", type=float, default=2.0,
+                    help="device-wait timeout (s) of the start-up canary replay (0: no canary)")
     ap.add_argument("--graph-chunk", type=int, default=0,
                     help="iterations per hipGraph (0 = the solver's choice: 32, 96 for the overlapped N > 1 schedule)")
     ap.add_argument("--converge-eps", type=float, default=1e-5,
@@ -212,15 +218,6 @@ def run_rank(args) -> int:
         return 2
     dev = info.local_rank % ndev
     runtime = heat3d_amd.runtime()
-    # Ranks per GPU (rehearsals put a whole node's ranks on one device): the
-    # overlapped schedule's per-stream graphs wait across streams with
-    # spinning device-side kernels, which assume the process's hardware queues
-    # stay resident.  Eight processes on one GPU oversubscribe its queues and
-    # the 8-rank rehearsal hung in its warm-up (gpurun_out/r8f), eager it ran
-    # (r8g); 2-4 processes on one GPU run the graphs (tests/test_gpu_rccl.py).
-    # So more than 4 ranks per device replay eagerly; one per GPU never does.
-    per_dev = -(-int(os.environ.get("LOCAL_WORLD_SIZE", world)) // ndev)
-    stream_graphs = per_dev <= 4
 
     G = args.grid
     N = (G, G, G)
@@ -256,8 +253,8 @@ def run_rank(args) -> int:
                           decomp=dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
                           device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
-                          extra_args=([] if stream_graphs else ["--no-stream-graphs"]) +
-                                     ["--temporal", str(args.temporal), "--kernel2", args.kernel2,
+                          extra_args=["--stream-graphs", args.stream_graphs, "--graph-canary", str(args.graph_canary),
+                                      "--temporal", str(args.temporal), "--kernel2", args.kernel2,
                                       "--watchdog", str(args.watchdog), "--reserve-cus", str(args.reserve_cus)]
                           + list(extra))
 
@@ -319,6 +316,8 @@ def run_rank(args) -> int:
     value = points * args.steps / dt / 1e9
     esize = 8 if args.dtype == "fp64" else 4
     kernel = s.kernel
+    sg_state, sg_note = s.native.stream_graphs_state, s.native.stream_graphs_note
+    per_dev = s.native.ranks_per_device
     comm_name = s.native.comm_name
     comm_ranks = s.native.comm_transport_ranks
     nbuf = s.native.field_buffers
@@ -386,7 +385,10 @@ def run_rank(args) -> int:
                    + (f" ({args.virtual_ranks} virtual ranks on 1 GPU)" if args.virtual_ranks > 1 else ""),
                    "kernel": kernel, "temporal_K": K, "field_buffers": nbuf,
                    "graph_requested": not args.no_graph, "graph_used": graph_launches > 0,
-                   "stream_graphs": stream_graphs, "ranks_per_device": per_dev,
+                   # the overlapped schedule's per-stream graphs as the start-up canary
+                   # left them (on / fallback / off / n/a; Solver::canary_stream_graphs)
+                   "stream_graphs": sg_state, "stream_graphs_canary": sg_note,
+                   "ranks_per_device": per_dev,
                    "graph_launches": graph_launches,
                    "overlap": not args.no_overlap, "comm": comm_name, "reserved_cus": reserved,
                    "preheat_sweeps": preheat},

@@ -140,6 +140,14 @@ static int drive(const Config& cfg, Solver& solver) {
     j.set("error_percent", 100.0 * gerr);
     j.set("error_percent_rank0_local", 100.0 * lerr);
     j.set_bool("fault", r.fault);
+    j.set("graph_launches", (int64_t)solver.graph_launches());
+    j.set("stream_graphs", solver.stream_graphs_state());
+    j.set("stream_graphs_canary", solver.stream_graphs_note());
+    const HipRuntimeInfo hi = solver.backend().is_gpu() ? hip_runtime_info() : HipRuntimeInfo{};
+    j.set("hip_runtime_version", (int64_t)hi.runtime_version);
+    j.set("hip_library", hi.library);
+    j.set("rccl_version", rccl_version());
+    j.set("rccl_library", rccl_library_path());
     io::write_file_atomic(cfg.json_out, j.dump() + "\n");
   }
   return r.fault ? 3 : 0;

@@ -121,8 +121,12 @@ std::string Config::usage() {
      << "                            GPU only, measure = on any backend)\n"
      << "  --autotune auto|on|off    time the sweep schedule candidates (z stride, x segments) at start-up;\n"
      << "                            auto: single-subdomain runs (--no-autotune = off)\n"
-     << "  --no-stream-graphs        run the overlapped multi-stream schedule eagerly (default: one linear\n"
-     << "                            hipGraph per stream, device-side cross-stream waits)\n"
+     << "  --stream-graphs auto|on|off  the overlapped multi-stream schedule as one linear hipGraph per\n"
+     << "                            stream with device-side cross-stream waits (auto: on unless more than\n"
+     << "                            4 ranks share a GPU; --no-stream-graphs = off), verified at start-up\n"
+     << "  --graph-canary S          device-wait timeout of the start-up canary replay of those graphs; a\n"
+     << "                            rank whose replay times out or runs > 2x eager turns them off for the\n"
+     << "                            job (default 2; 0 = no canary)\n"
      << "  --no-rccl-graph           never record RCCL calls into hipGraphs (eager multi-rank steps)\n"
      << "  --rccl-shared             one RCCL communicator for halos and all-reduces\n"
      << "  --rccl-p2p-channels N     RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS unless set in the\n"
@@ -268,8 +272,13 @@ Config Config::parse(int argc, const char* const* argv) {
       else if (v == "off") c.autotune = 0;
       else throw UsageError("--autotune auto|on|off, not '" + v + "'");
     }
-    else if (key == "--no-stream-graphs") c.stream_graphs = false;
-    else if (key == "--stream-graphs") c.stream_graphs = true;
+    else if (key == "--no-stream-graphs") c.stream_graphs = 0;
+    else if (key == "--stream-graphs") {
+      const std::string v = get("--stream-graphs");
+      if (v != "auto" && v != "on" && v != "off") throw UsageError("--stream-graphs auto|on|off");
+      c.stream_graphs = v == "auto" ? -1 : v == "on" ? 1 : 0;
+    }
+    else if (key == "--graph-canary") c.graph_canary_s = to_f64(get("--graph-canary"), "--graph-canary");
     else if (key == "--rccl-graph") c.rccl_graph = true;
     else if (key == "--no-rccl-graph") c.rccl_graph = false;
     else if (key == "--rccl-shared") c.rccl_shared = true;

@@ -86,8 +86,14 @@ struct Config {
   // time the interior sweeps' schedule candidates at initialisation: -1 auto
   // (single-subdomain runs, whose sweeps run alone as they are timed), 0 off, 1 on
   int autotune = -1;
-  bool stream_graphs = true;      // overlapped multi-stream schedules as hipGraphs too (one linear graph
-                                  // per stream; --no-stream-graphs: eager)
+  // overlapped multi-stream schedules as hipGraphs too (one linear graph per
+  // stream, device-side cross-stream waits): -1 auto (on unless more than 4
+  // ranks share a GPU: oversubscribed hardware queues), 1 on, 0 eager.  Where
+  // on, a canary replay at initialisation with a short device-wait timeout
+  // (graph_canary_s) decides; a timed-out or pathologically slow replay on any
+  // rank turns them off for the job (Solver::canary_stream_graphs).
+  int stream_graphs = -1;
+  double graph_canary_s = 2.0;    // device-wait timeout of the canary replay (0: no canary)
   bool rccl_graph = true;         // RCCL calls may be recorded into hipGraphs (tests/test_gpu_rccl.py)
   bool rccl_shared = false;       // one RCCL communicator for halos and all-reduces (else ncclCommSplit)
   int rccl_p2p_channels = 0;      // RCCL P2P channel pool: 0 auto (the reserved CUs, 8), -1 RCCL's default
@@ -102,8 +108,8 @@ struct Config {
   int phantom_channels = 4;       // workgroups an emulated transfer holds per peer
   int phantom_allreduce_channels = 2;
   bool phantom_overlap = false;   // --phantom-wire overlap: copies inside the emulated wire time
-  bool phantom_paced = false;
-  bool phantom_rccl_footprint = false;  // --phantom-footprint rccl|small: stand-in kernels sized as RCCL's     // --phantom-wire paced: copies paced at the wire rate for the wire time
+  bool phantom_paced = false;     // --phantom-wire paced: copies paced at the wire rate for the wire time
+  bool phantom_rccl_footprint = false;  // --phantom-footprint rccl|small: stand-in kernels sized as RCCL's
 
   // Parse argv.  Throws UsageError on a malformed command line.
   static Config parse(int argc, const char* const* argv);

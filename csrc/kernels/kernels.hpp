@@ -156,7 +156,7 @@ void cu_probe(unsigned* out, int blocks, double us, void* stream);
 // then a no-op) and returns, so a broken dependency cannot hang the GPU.
 void graph_signal(unsigned* slot, void* stream);
 // (wait: on every one of `n` <= 4 slots)
-void graph_wait(const unsigned* const* slots, int n, DeviceState* st, double timeout_s, void* stream);
+void graph_wait(const unsigned* const* slots, int n, DeviceState* st, void* stream);
 // Adds Σ|T - y| and the point count over `box` into s->error_sum/error_count.
 // `scratch` must hold at least error_scratch_elems() doubles.
 void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,

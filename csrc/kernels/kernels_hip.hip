@@ -779,19 +779,29 @@ struct WaitSlots {
   const unsigned* p[4];
 };
 
-__global__ void graph_wait_kernel(WaitSlots w, int n, DeviceState* st, unsigned long long ticks) {
+// Waits for 1..4 signal slots of other streams' graphs.  Polls with relaxed
+// agent-scope loads (an acquire load invalidates the L2 lines of the XCD at
+// every poll, under an interior sweep that lives on L2 hits) and sleeps
+// between polls; one acquire fence once every slot has flipped.  Gives up
+// after st->wait_ticks (100 MHz) and flags fault 2 + done, and a wait that
+// finds the fault already flagged returns at once, so one broken dependency
+// drains the rest of the graph in one timeout.
+__global__ void graph_wait_kernel(WaitSlots w, int n, DeviceState* st) {
   if (threadIdx.x != 0) return;
+  if (__hip_atomic_load(&st->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 2) return;
+  const unsigned long long ticks = __hip_atomic_load(&st->wait_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (int i = 0; i < n; ++i) {
-    while (__hip_atomic_load(w.p[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+    while (__hip_atomic_load(w.p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
         __hip_atomic_store(&st->fault, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&st->done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(4);
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 void graph_signal(unsigned* slot, void* stream) {
@@ -799,12 +809,11 @@ void graph_signal(unsigned* slot, void* stream) {
   HIPK_CHECK(hipGetLastError());
 }
 
-void graph_wait(const unsigned* const* slots, int n, DeviceState* st, double timeout_s, void* stream) {
+void graph_wait(const unsigned* const* slots, int n, DeviceState* st, void* stream) {
   HEAT3D_CHECK(n >= 1 && n <= 4 && st, "graph_wait: 1..4 slots and a state");
   WaitSlots w{};
   for (int i = 0; i < n; ++i) w.p[i] = slots[i];
-  hipLaunchKernelGGL(graph_wait_kernel, dim3(1), dim3(64), 0, S(stream), w, n, st,
-                     (unsigned long long)(timeout_s * 1e8));  // 100 MHz real-time clock
+  hipLaunchKernelGGL(graph_wait_kernel, dim3(1), dim3(64), 0, S(stream), w, n, st);
   HIPK_CHECK(hipGetLastError());
 }
 

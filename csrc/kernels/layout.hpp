@@ -76,7 +76,10 @@ struct DeviceState {
   int64_t iter;                    // iterations checked so far (next index)
   int64_t conv_iter;               // 0-based converged iteration, -1 until then
   int32_t done;                    // convergence reached (or fault): stencils early-exit
-  int32_t fault;                   // 1 = NaN/Inf residual detected
+  int32_t fault;                   // 1 = NaN/Inf residual detected, 2 = a graph wait timed out
+  // device-side cross-stream waits of per-stream hipGraphs give up after this
+  // many 100 MHz ticks (read at every wait: the start-up canary shortens it)
+  uint64_t wait_ticks;
   int64_t hist_cap;                // residual history ring capacity
   double hist[1024];               // residual history ring (index = iter % cap)
 };

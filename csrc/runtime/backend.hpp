@@ -76,15 +76,12 @@ class Backend {
   //     priority kept); a wait on an event another stream recorded inside
   //     the recording becomes a device-side wait on a signal slot, set by
   //     the recording stream (kernels graph_signal / graph_wait).  A wait
-  //     that times out (set_graph_wait_timeout) marks `fault_state`
-  //     (fault = 2, done = 1).
+  //     that outlasts fault_state->wait_ticks (read when it runs) marks
+  //     `fault_state` (fault = 2, done = 1).
   // launch_graph joins every stream into the compute stream afterwards.
   virtual bool supports_graphs() const { return false; }
   virtual void begin_capture(bool /*per_stream*/ = false, DeviceState* /*fault_state*/ = nullptr,
                              int /*max_signals*/ = 0) {}
-  // how long a device-side wait of a per-stream graph may spin before it
-  // flags the fault (s; the solver passes its --watchdog)
-  virtual void set_graph_wait_timeout(double /*seconds*/) {}
   virtual void* end_capture() { return nullptr; }  // returns executable graph
   virtual void launch_graph(void* /*exec*/) {}
   virtual void destroy_graph(void* /*exec*/) {}
@@ -136,7 +133,7 @@ std::unique_ptr<Backend> make_cpu_backend(int threads);
 std::unique_ptr<Backend> make_hip_backend(int device);
 int hip_device_count();  // 0 when no GPU / no driver
 // The HIP runtime this process is bound to: hipRuntimeGetVersion (e.g.
-// 70253121 = 7.2.53121) and the file libamdhip64.so.7 resolved to.  PyTorch
+// 70226015 = 7.2.26015) and the file libamdhip64.so.7 resolved to.  PyTorch
 // bundles a HIP 7.0 runtime under the same soname: a process that imports
 // torch before the solver runs on torch's copy (bench.py and smoke() do not).
 struct HipRuntimeInfo {

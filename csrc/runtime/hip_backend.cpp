@@ -313,7 +313,6 @@ class HipBackend final : public Backend {
   }
 
   bool supports_graphs() const override { return true; }
-  void set_graph_wait_timeout(double s) override { wait_timeout_s_ = s > 0 ? s : 300.0; }
   void begin_capture(bool per_stream, DeviceState* fault_state, int max_signals) override {
     HEAT3D_CHECK(!recording_, "graph recording already active");
     split_ = per_stream;
@@ -497,7 +496,7 @@ class HipBackend final : public Backend {
         } else {
           const unsigned* p[4];
           for (std::size_t i = 0; i < it.slots.size(); ++i) p[i] = sig_ + it.slots[i];
-          hip::graph_wait(p, (int)it.slots.size(), fault_, wait_timeout_s_, st);
+          hip::graph_wait(p, (int)it.slots.size(), fault_, st);
         }
       } catch (...) {
         abort_op();
@@ -506,10 +505,6 @@ class HipBackend final : public Backend {
       op_end(s);
     }
   }
-  // a device-side wait longer than this is a broken dependency (or a peer
-  // that stopped): the kernel gives up and flags the fault instead of
-  // holding the GPU (the solver's --watchdog)
-  double wait_timeout_s_ = 300.0;
   struct GraphSet {
     bool per_stream = false;
     hipGraphExec_t ex[kNumStreams] = {nullptr, nullptr, nullptr};

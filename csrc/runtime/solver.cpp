@@ -265,7 +265,20 @@ Solver::Solver(const Config& cfg, std::unique_ptr<Backend> be, std::unique_ptr<C
     slot_stride_ = K_ + (long_halo_ ? 1 : 0);
   }
   fake_allreduce_us_ = cfg_.fake_allreduce_us;
-  be_->set_graph_wait_timeout(cfg_.watchdog_s);
+  // processes sharing this rank's GPU: the launcher's local world size over
+  // the visible devices (one process hosting virtual ranks counts once)
+  if (be_->is_gpu() && !comm_->all_local()) {
+    int local = 0;
+    for (const char* v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"}) {
+      const char* e = std::getenv(v);
+      if (e && *e) {
+        local = std::atoi(e);
+        break;
+      }
+    }
+    const int ndev = std::max(1, hip_device_count());
+    ranks_per_device_ = std::max(1, (local + ndev - 1) / ndev);
+  }
   chain_ = comm_->ordered_collectives() && !comm_->all_local() && comm_->size() > 1;
   // a long x-slab interior (the 2-GPU 1024^3 share): the halo chain hides
   // under it with room to spare (no CU reservation)
@@ -547,13 +560,7 @@ void Solver::initialize() {
   be_->sync_all();
   destroy_graphs();
   pending_.valid = false;
-  for (auto& l : local_) {
-    InitParams p = init_params(l);
-    for (int b = 0; b < nbuf_; ++b) {
-      p.field = l.field[b];
-      be_->init_field(dt_, p, kCompute);
-    }
-  }
+  init_fields();
   sweep_costs_.clear();
   if (pick_sweep_form()) {  // re-timed from the lean form on every initialisation
     KernelSpec lean;
@@ -563,6 +570,21 @@ void Solver::initialize() {
   }
   tune_schedules();
   calibrate_remainders();
+  reset_state();
+  canary_stream_graphs();
+}
+
+void Solver::init_fields() {
+  for (auto& l : local_) {
+    InitParams p = init_params(l);
+    for (int b = 0; b < nbuf_; ++b) {
+      p.field = l.field[b];
+      be_->init_field(dt_, p, kCompute);
+    }
+  }
+}
+
+void Solver::reset_state() {
   DeviceState hs;
   std::memset(&hs, 0, sizeof(hs));
   for (auto& r : hs.residual) r = kResidualInitBits;
@@ -571,6 +593,9 @@ void Solver::initialize() {
   hs.iter = 0;
   hs.conv_iter = -1;
   hs.hist_cap = 1024;
+  // a device-side graph wait longer than the watchdog is a broken dependency
+  // or a stalled peer: the kernel flags it instead of holding the GPU
+  hs.wait_ticks = (uint64_t)(cfg_.watchdog_s * 1e8);
   std::memcpy(hstate_, &hs, sizeof(hs));
   be_->copy(dstate_, hstate_, sizeof(DeviceState), CopyKind::H2D, kCompute);
   be_->sync(kCompute);
@@ -581,6 +606,7 @@ void Solver::initialize() {
   last_bnd_ = 0;
   segs_.clear();
   seg_head_ = 0;
+  sg_unchecked_ = false;
   if (!cfg_.restart.empty()) load_checkpoint(cfg_.restart);
   // make every pipeline event valid (complete) before the first iteration
   for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
@@ -591,6 +617,99 @@ void Solver::initialize() {
   }
   be_->sync_all();
   comm_->barrier(*be_);
+}
+
+void Solver::set_wait_timeout(double seconds) {
+  const uint64_t t = (uint64_t)(seconds * 1e8);  // 100 MHz real-time clock
+  hstate_->wait_ticks = t;
+  be_->copy(reinterpret_cast<char*>(dstate_) + offsetof(DeviceState, wait_ticks), &hstate_->wait_ticks,
+            sizeof(uint64_t), CopyKind::H2D, kCompute);
+  be_->sync(kCompute);
+}
+
+void Solver::check_graph_fault() {
+  if (!sg_unchecked_) return;
+  sg_unchecked_ = false;
+  int32_t f = 0;
+  be_->copy(&f, reinterpret_cast<char*>(dstate_) + offsetof(DeviceState, fault), sizeof(int32_t), CopyKind::D2H,
+            kCompute);
+  be_->sync(kCompute);
+  HEAT3D_CHECK(f != 2, "a device-side wait of a per-stream hipGraph timed out after "
+                           << cfg_.watchdog_s << " s (broken dependency or a stalled peer)");
+}
+
+// Per-stream graphs replace cross-stream events by spinning one-wave wait
+// kernels on the consumer's stream.  They hold only while each stream keeps a
+// hardware queue of its own: a wait queued behind the work it waits for on a
+// shared queue never ends (the 8-ranks-on-one-GPU rehearsal hung that way,
+// round 5).  Nothing in HIP reports the queue mapping, so the schedule is
+// tried once, at start-up, with a short timeout, and kept only if it ran.
+void Solver::canary_stream_graphs() {
+  sg_note_.clear();
+  if (!multi_stream() || !be_->supports_graphs()) {
+    sg_state_ = "n/a";
+    return;
+  }
+  if (!graphs_allowed()) {
+    sg_state_ = sg_fallback_ ? "fallback" : "off";
+    return;
+  }
+  if (cfg_.graph_canary_s <= 0) {
+    sg_state_ = "unverified";
+    return;
+  }
+  const int64_t cyc = tb_ ? (int64_t)K_ * (nbuf_ == 3 ? 6 : 2) : (nbuf_ == 3 ? 6 : 2);
+  const int G = graph_len_for(cyc);
+  if (G <= 0) {
+    sg_state_ = "unverified";
+    return;
+  }
+  set_wait_timeout(cfg_.graph_canary_s);
+  force_eager_ = true;
+  comm_->barrier(*be_);
+  double t0 = now_s();
+  run_chunk(G);
+  be_->sync_all();
+  const double eager = now_s() - t0;
+  force_eager_ = false;
+  prepare_steps(G);
+  const int64_t launches = graph_launches_;
+  comm_->barrier(*be_);
+  t0 = now_s();
+  run_chunk(G);
+  be_->sync_all();
+  const double graph = now_s() - t0;
+  sg_unchecked_ = false;
+  be_->copy(hstate_, dstate_, offsetof(DeviceState, hist), CopyKind::D2H, kCompute);
+  be_->sync(kCompute);
+  const bool timed_out = hstate_->fault == 2;
+  const bool replayed = graph_launches_ > launches;
+  const bool slow = graph > 2.0 * eager + 1e-3;
+  // one decision for the job: the ranks' schedules must stay the same kind
+  // (their collectives pair up either way, but a mixed job has no use)
+  const unsigned long long vote =
+      allreduce_sum_u64((timed_out ? 1ull << 40 : 0ull) + (slow ? 1ull << 20 : 0ull) + (replayed ? 0ull : 1ull));
+  std::ostringstream os;
+  os.setf(std::ios::fixed);
+  os.precision(3);
+  os << G << " iterations: graphs " << graph * 1e3 << " ms, eager " << eager * 1e3 << " ms";
+  if (vote >> 40) os << "; " << (vote >> 40) << " rank(s) timed out in a device-side wait";
+  if ((vote >> 20) & 0xfffff) os << "; " << ((vote >> 20) & 0xfffff) << " rank(s) replayed > 2x eager";
+  if (vote & 0xfffff) os << "; " << (vote & 0xfffff) << " rank(s) did not replay a graph";
+  sg_note_ = os.str();
+  if (vote) {
+    sg_fallback_ = true;
+    sg_state_ = "fallback";
+    destroy_graphs();
+    if (!cfg_.quiet && is_root())
+      std::fprintf(stderr, "heat3d: per-stream hipGraph canary failed (%s); the overlapped schedule runs eagerly\n",
+                   sg_note_.c_str());
+  } else {
+    sg_state_ = "on";
+  }
+  // back to iteration 0 (reset_state restores the watchdog-long wait timeout)
+  init_fields();
+  reset_state();
 }
 
 // Time the x-schedule candidates of every interior sweep shape this run will
@@ -1452,7 +1571,15 @@ bool Solver::graphs_allowed() const {
   // replayed by the HIP runtime on streams of its own without either: 0.366
   // against 0.212 ms/step eager on the 8-GPU slab share, profiles/rank_proxy_r04.md.)
   return cfg_.use_graph && be_->supports_graphs() && comm_->capturable() && !graph_failed_ && !phase_timing_ &&
-         (!multi_stream() || cfg_.stream_graphs);
+         !force_eager_ && (!multi_stream() || stream_graphs_enabled());
+}
+
+// --stream-graphs auto: on unless more than 4 processes share the GPU (the
+// 8-rank one-GPU rehearsal oversubscribed its hardware queues and hung with
+// them, round 5); the canary has the last word either way
+bool Solver::stream_graphs_enabled() const {
+  if (sg_fallback_ || cfg_.stream_graphs == 0) return false;
+  return cfg_.stream_graphs == 1 || ranks_per_device_ <= 4;
 }
 
 Solver::GraphEntry* Solver::find_graph(int G) {
@@ -1586,6 +1713,7 @@ void Solver::run_chunk(int64_t n) {
         join_pipeline();
         be_->launch_graph(g->exec);
         ++graph_launches_;
+        if (multi_stream()) sg_unchecked_ = true;
         if (g->kind == 2) {
           for (int i = 0; i < G / K_; ++i) {
             record_segment(issued_, K_, cur());
@@ -1644,6 +1772,7 @@ void Solver::step(int64_t n) { run_chunk(n); }
 void Solver::synchronize() {
   be_->sync_all();
   comm_->check_async_error();
+  check_graph_fault();
 }
 
 HostState Solver::state() {

@@ -105,6 +105,15 @@ class Solver {
   int64_t iterations_issued() const { return issued_; }
   // hipGraph launches so far (what actually ran, not the --graph request)
   int64_t graph_launches() const { return graph_launches_; }
+  // The overlapped multi-stream schedule's per-stream hipGraphs: "n/a" (a
+  // single-stream schedule), "off" (requested off, graphs off, or more than 4
+  // ranks per GPU under auto), "on" (canary passed; details in
+  // stream_graphs_note()), "unverified" (--graph-canary 0) or "fallback" (the
+  // canary timed out or ran > 2x eager on some rank: eager for the job).
+  const std::string& stream_graphs_state() const { return sg_state_; }
+  const std::string& stream_graphs_note() const { return sg_note_; }
+  // processes sharing this rank's GPU, as the launcher's environment tells
+  int ranks_per_device() const { return ranks_per_device_; }
 
   // Error vs analytic steady state (heat3D.cu:1093-1106, with a true global
   // mean instead of rank-0's local value).  Uses the current field.
@@ -228,6 +237,21 @@ class Solver {
   };
 
   void setup_faces();
+  // initialize(): the analytic IC (or nothing, before a restart) into every
+  // field buffer, and the device state / schedule counters / events of
+  // iteration 0 (restart: of the checkpoint)
+  void init_fields();
+  void reset_state();
+  // Start-up canary of the per-stream graphs (initialize(), every rank at the
+  // same point): one schedule cycle eagerly, then the same cycle as per-stream
+  // graphs with the device-side waits' timeout cut to --graph-canary; a
+  // timed-out wait or a replay > 2x the eager time on any rank (one vote)
+  // turns the graphs off for the job.  The fields are re-initialised after.
+  void canary_stream_graphs();
+  void set_wait_timeout(double seconds);
+  bool stream_graphs_enabled() const;
+  // fault 2 (a timed-out device-side wait) after per-stream graph launches
+  void check_graph_fault();
   // one single-step iteration: residual slot / event parity p, input buffer bi
   void enqueue_iteration(int p, int bi);
   // K iterations in one temporally blocked sweep from buffer bi
@@ -360,6 +384,11 @@ class Solver {
   std::vector<GraphEntry> graphs_;  // small cache, keyed by (G, kind, buf, parities)
   bool graph_failed_ = false;
   int64_t graph_launches_ = 0;
+  bool force_eager_ = false;        // canary: the eager reference chunk
+  bool sg_fallback_ = false;        // the canary turned the per-stream graphs off (sticky)
+  bool sg_unchecked_ = false;       // per-stream graphs launched since the last fault check
+  int ranks_per_device_ = 1;
+  std::string sg_state_ = "n/a", sg_note_;
 
   bool phase_timing_ = false;
   std::vector<std::pair<std::string, double>> phase_acc_;

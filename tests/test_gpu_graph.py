@@ -61,24 +61,89 @@ def test_short_bench_replays_graph(h3d, gpu):
 
 
 def test_stream_graph_wait_timeout_flags_fault(h3d, gpu):
-    """The safety net of the per-stream graphs: a device-side cross-stream
-    wait that outlasts --watchdog gives up, sets fault = 2 and the done flag
-    (later sweeps are no-ops) instead of holding the GPU.  A phantom rank
-    whose emulated halo takes ~3 s (a link of 4e-5 GB/s) makes the compute
-    stream's wait for the boundary slabs exceed a 0.5 s watchdog."""
+    """The safety net of the per-stream graphs in steady state: a device-side
+    cross-stream wait that outlasts --watchdog gives up, sets fault = 2 and
+    the done flag (later sweeps are no-ops) instead of holding the GPU, and
+    synchronize() raises.  A phantom rank whose emulated halo takes ~3 s (a
+    link of 4e-5 GB/s) makes the compute stream's wait for the boundary slabs
+    exceed a 0.5 s watchdog.  (--graph-canary 0: no start-up canary, which
+    would have turned the graphs off.)"""
     import time
 
     s = h3d.HeatSolver((64, 64, 64), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(1, 8),
                        graph_chunk=6,
                        extra_args=["--phantom-gbps", "4e-5", "--phantom-allreduce-us", "1", "--watchdog", "0.5",
-                                   "--long-sweeps", "off"])
+                                   "--long-sweeps", "off", "--lag", "off", "--graph-canary", "0"])
     s.initialize()
+    assert s.native.stream_graphs_state == "unverified"
     g0 = s.native.graph_launches
     t0 = time.perf_counter()
     s.step(6)   # one graph of two sweeps: the second interior waits for the first boundary slabs
-    s.synchronize()
+    with pytest.raises(RuntimeError, match="timed out"):
+        s.synchronize()
     el = time.perf_counter() - t0
     assert s.native.graph_launches - g0 == 1
     st = s.state()
     assert st["fault"] == 2 and st["done"] == 1, st
     assert el < 60, el   # the two emulated halos (~3 s each) end, nothing waits for ever
+
+
+def test_stream_graph_canary_falls_back_to_eager(h3d, gpu):
+    """The start-up canary: a per-stream graph replay whose device-side wait
+    outlasts --graph-canary (an emulated halo of ~0.6 s against 0.2 s) turns
+    the graphs off in the same process; the solver re-initialises and the run
+    continues eagerly and correctly — no hang, no fault, no graph launch."""
+    import time
+
+    args = ["--phantom-gbps", "2e-4", "--phantom-allreduce-us", "1", "--long-sweeps", "off", "--lag", "off"]
+    t0 = time.perf_counter()
+    s = h3d.HeatSolver((64, 64, 64), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(1, 8),
+                       graph_chunk=6, extra_args=args + ["--graph-canary", "0.2"])
+    s.initialize()
+    el = time.perf_counter() - t0
+    assert s.native.stream_graphs_state == "fallback", s.native.stream_graphs_note
+    assert "timed out" in s.native.stream_graphs_note
+    assert el < 60, el
+    st = s.state()
+    assert st["iter"] == 0 and st["fault"] == 0 and st["done"] == 0, st
+    g0 = s.native.graph_launches
+    s.step(6)
+    s.synchronize()
+    assert s.native.graph_launches == g0
+    st = s.state()
+    assert st["iter"] == 6 and st["fault"] == 0 and st["done"] == 0, st
+    # the same steps with graphs off from the start: the same field
+    e = h3d.HeatSolver((64, 64, 64), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(1, 8),
+                       graph_chunk=6, extra_args=args + ["--no-stream-graphs"])
+    e.initialize()
+    assert e.native.stream_graphs_state == "off"
+    e.step(6)
+    e.synchronize()
+    import numpy as np
+
+    assert np.array_equal(s.local_field(0, True), e.local_field(0, True))
+
+
+def test_stream_graph_canary_passes(h3d, gpu):
+    """A healthy phantom rank: the canary replays, keeps the graphs, and the
+    timed steps replay them; the field after the canary is the initial one."""
+    import numpy as np
+
+    args = ["--phantom-gbps", "50", "--long-sweeps", "off"]
+    s = h3d.HeatSolver((96, 96, 96), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(2, 8),
+                       extra_args=args)
+    s.initialize()
+    assert s.native.stream_graphs_state == "on", s.native.stream_graphs_note
+    assert "graphs" in s.native.stream_graphs_note and "eager" in s.native.stream_graphs_note
+    st = s.state()
+    assert st["iter"] == 0 and st["fault"] == 0, st
+    g0 = s.native.graph_launches
+    s.step(36)
+    s.synchronize()
+    assert s.native.graph_launches > g0
+    e = h3d.HeatSolver((96, 96, 96), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(2, 8),
+                       extra_args=args + ["--no-graph"])
+    e.initialize()
+    e.step(36)
+    e.synchronize()
+    assert np.array_equal(s.local_field(0, True), e.local_field(0, True))
