@@ -61,10 +61,12 @@ def parse_args(argv=None):
                          "(BASELINE config 5: B=2047 fp32 gives 4096^3 on 8 GPUs)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--decomp", default="auto",
-                    help="auto | slab | block | AxBxC.  auto: slabs, unless the start-up link probe (a K-deep "
-                         "face to both ring neighbours through the job's transport, slowest rank) measures "
-                         "less than the phantom-rank proxy's crossover (8 ranks: 55 GB/s), then 2D blocks")
-    ap.add_argument("--no-link-probe", action="store_true", help="--decomp auto without the link probe: slabs")
+                    help="auto | slab | block | AxBxC.  auto (N > 1): each candidate grid (x slabs, 2D and 3D "
+                         "blocks: parallel.decomp_candidates) runs --decomp-trial-steps timed steps of the "
+                         "production schedule through the job's transport at start-up; the fastest by its "
+                         "slowest rank is kept (JSON decomp_auto)")
+    ap.add_argument("--decomp-trial-steps", type=int, default=36,
+                    help="steps per timed window of each --decomp auto candidate (best of 3; 0: slabs untimed)")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
@@ -191,7 +193,7 @@ def run_rank(args) -> int:
     os.environ.setdefault("HEAT3D_RUNTIME", "rocm")
     import heat3d_amd
     from heat3d_amd import HeatSolver
-    from heat3d_amd.parallel import SLAB_MIN_LINK_GBPS, best_dims_for, choose_dims
+    from heat3d_amd.parallel import best_dims_for, decomp_candidates, pick_measured
     from heat3d_amd.parallel.distributed import (HostGroup, all_gather_objects, barrier, env_info,
                                                  max_over_ranks)
     from heat3d_amd.utils.metrics import roofline_glups
@@ -224,39 +226,61 @@ def run_rank(args) -> int:
     nparts = world * args.virtual_ranks
     if args.virtual_ranks > 1:
         assert world == 1, "--virtual-ranks is a single-process diagnostic"
-    link = None
-    if args.decomp == "auto" and world > 1 and args.virtual_ranks == 1 and not args.no_link_probe:
-        # time one K-deep x face (the slab halo of a sweep) to both ring
-        # neighbours over the job's own transport, on a throw-away solver
-        # whose communicator is created like the real one; every rank gets
-        # the slowest rank's rate
-        esize = 8 if args.dtype == "fp64" else 4
-        depth = args.temporal if args.temporal >= 2 else 3
-        face = depth * (G + 2) * (G + 8) * esize
-        probe = HeatSolver((4 * world + 2, 8, 8), iter_max=1, eps=0.0, dtype=args.dtype, backend="hip",
-                           decomp=(world, 1, 1), device=dev, group=group, comm=args.comm,
-                           extra_args=["--watchdog", str(args.watchdog)])
-        link = probe.native.link_probe(face, 5)
-        del probe
-        dims = choose_dims(N, nparts, link)
+    trials = None
+    if args.decomp == "auto" and world > 1 and args.virtual_ranks == 1 and args.decomp_trial_steps > 0 \
+            and not args.weak_block:
+        dims, trials = None, []
     elif args.decomp in ("auto", "slab", "block"):
         dims = best_dims_for(N, nparts, None if args.decomp == "auto" else args.decomp)
     else:
         dims = tuple(int(v) for v in args.decomp.lower().split("x"))
-    assert dims[0] * dims[1] * dims[2] == nparts, (dims, nparts)
-    if args.weak_block:
-        N = tuple(d * args.weak_block + 2 for d in dims)
-        G = N[0]
 
-    def make(eps, iter_max, extra=()):
+    def make(eps, iter_max, extra=(), decomp=None):
         return HeatSolver(N, iter_max=iter_max, eps=eps, dtype=args.dtype, backend="hip",
-                          decomp=dims, kernel=args.kernel, graph=not args.no_graph,
+                          decomp=decomp or dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
                           device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
                           extra_args=["--stream-graphs", args.stream_graphs, "--graph-canary", str(args.graph_canary),
                                       "--temporal", str(args.temporal), "--kernel2", args.kernel2,
                                       "--watchdog", str(args.watchdog), "--reserve-cus", str(args.reserve_cus)]
                           + list(extra))
+
+    if trials is not None:
+        # --decomp auto: time each candidate process grid (x slabs, 2D, 3D
+        # blocks) through the job's own transport — the production schedule
+        # (overlapped sweeps, graphs as configured) from the initial state —
+        # and keep the fastest by the slowest rank's time (one decision: every
+        # rank gets the same maxima).  The reference takes MPI_Dims_create's
+        # grid by rank count alone (heat3D.cu:243).
+        esteps = args.decomp_trial_steps
+        cands = decomp_candidates(N, nparts, args.temporal if args.temporal >= 2 else 3)
+        if len(cands) == 1:
+            dims, trials = cands[0], None
+            cands = []
+        for d in cands:
+            t = make(0.0, 1 << 40, decomp=d)
+            t.initialize()
+            t.step(esteps)
+            t.prepare_steps(esteps)
+            t.synchronize()
+            best = None
+            for _ in range(3):
+                barrier(group)
+                t0 = time.perf_counter()
+                t.step(esteps)
+                t.synchronize()
+                dt1 = time.perf_counter() - t0
+                best = dt1 if best is None else min(best, dt1)
+            ms = max_over_ranks(best, group) / esteps * 1e3
+            trials.append({"dims": list(d), "ms_per_step": round(ms, 4),
+                           "stream_graphs": t.native.stream_graphs_state})
+            del t
+        if trials:
+            dims = pick_measured(trials)
+    assert dims[0] * dims[1] * dims[2] == nparts, (dims, nparts)
+    if args.weak_block:
+        N = tuple(d * args.weak_block + 2 for d in dims)
+        G = N[0]
 
     phase_log = os.environ.get("HEAT3D_BENCH_PHASES") == "1"
     tp = [time.perf_counter()]
@@ -329,7 +353,6 @@ def run_rank(args) -> int:
     # K+1-step sweeps, from the start-up sweep timings (ms)
     placement = all_gather_objects({"rank": rank, "device": dev, "host": socket.gethostname(),
                                     "hip_library": runtime["hip_library"], "rccl_library": runtime["rccl_library"],
-                                    "link_probe_gbps": None if link is None else round(link, 3),
                                     "dims": list(dims), "rccl_p2p_channels": s.native.rccl_p2p_channels or None,
                                     "subdomain": list(s.native.local_subdomain(0)["n"]), "x_schedules": xs,
                                     "long_remainders": list(s.native.long_remainders),
@@ -393,11 +416,10 @@ def run_rank(args) -> int:
                    "overlap": not args.no_overlap, "comm": comm_name, "reserved_cus": reserved,
                    "preheat_sweeps": preheat},
         "comm_ranks": comm_ranks,
-        # --decomp auto: the start-up link probe (slowest rank's one-way GB/s
-        # per link) against the proxy's slab / 2D-block crossover
-        "decomp_auto": None if link is None else {"link_probe_gbps": round(link, 3),
-                                                   "slab_min_gbps": SLAB_MIN_LINK_GBPS.get(world),
-                                                   "dims": list(dims)},
+        # --decomp auto: every candidate grid's timed ms/step (slowest rank)
+        # and the one kept
+        "decomp_auto": None if not trials else {"trials": trials, "dims": list(dims),
+                                                "trial_steps": args.decomp_trial_steps},
         "placement": placement,
         "halo_verified": True,
         "headline_config": is_headline,

@@ -171,3 +171,38 @@ def choose_dims(N: Sequence[int], nprocs: int, link_gbps: Optional[float]) -> Tu
     if cut is None or link_gbps is None or link_gbps <= 0 or link_gbps >= cut or slab[0] != nprocs:
         return slab
     return (nprocs // 2, 2, 1)
+
+
+def decomp_candidates(N: Sequence[int], nprocs: int, K: int = 3) -> List[Tuple[int, int, int]]:
+    """Process grids the bench's ``--decomp auto`` times at start-up: x slabs,
+    the 2D block with two ranks along y, and the balanced 3D block
+    (MPI_Dims_create, heat3D.cu:243), in that order, without duplicates and
+    only where every split axis keeps an interior between its K-deep boundary
+    layers (>= 2K + 1 points: the overlapped sweep)."""
+    cands = [(nprocs, 1, 1)]
+    if nprocs % 2 == 0 and nprocs >= 4:
+        cands.append((nprocs // 2, 2, 1))
+    cands.append(dims_create(nprocs))
+    out: List[Tuple[int, int, int]] = []
+    for d in cands:
+        d = tuple(int(v) for v in d)
+        if d in out:
+            continue
+        if all(d[a] == 1 or (N[a] - 2) // d[a] >= 2 * K + 1 for a in range(3)):
+            out.append(d)  # type: ignore[arg-type]
+    return out
+
+
+def pick_measured(trials: Sequence[dict], margin: float = 0.02) -> Tuple[int, int, int]:
+    """The fastest timed candidate (``{"dims", "ms_per_step"}``, the slowest
+    rank's time each); a later candidate must beat the earlier pick by
+    ``margin`` (noise of short windows must not flip slabs to blocks)."""
+    best = None
+    for t in trials:
+        if t.get("ms_per_step") is None:
+            continue
+        if best is None or t["ms_per_step"] < best["ms_per_step"] * (1.0 - margin):
+            best = t
+    if best is None:
+        raise ValueError("no decomposition candidate was timed")
+    return tuple(best["dims"])  # type: ignore[return-value]

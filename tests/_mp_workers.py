@@ -3,6 +3,7 @@
 Each worker initialises torch.distributed (gloo, 127.0.0.1), runs a solver and
 saves its results to ``outdir`` so the parent test can compare them.
 """
+import json
 import os
 import sys
 
@@ -136,6 +137,9 @@ def native_rccl_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, ext
         np.save(os.path.join(outdir, "field.npy"), g)
         with open(os.path.join(outdir, "result.txt"), "w") as f:
             f.write(f"{r['conv_iter']} {r['error_percent']!r} {s.native.comm_name} {s.native.graph_launches}\n")
+        with open(os.path.join(outdir, "meta.json"), "w") as f:
+            json.dump({"dims": list(s.dims), "stream_graphs": s.native.stream_graphs_state,
+                       "stream_graphs_canary": s.native.stream_graphs_note}, f)
     else:
         assert g is None
     dist.barrier()

@@ -142,3 +142,55 @@ def test_rccl_graph_bitwise(h3d, gpu, tmp_path, world, decomp, schedule):
     assert int(graphs) > 0, "no hipGraph was replayed"
     assert int(it) == r1["conv_iter"] and name == "rccl"
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
+
+
+@pytest.mark.parametrize("decomp,dtype", [((2, 2, 2), "fp64"), ((2, 2, 2), "fp32"), ((4, 2, 1), "fp64"),
+                                          ((4, 2, 1), "fp32")])
+def test_rccl_8rank_blocks_bitwise(h3d, gpu, tmp_path, decomp, dtype):
+    """BASELINE configs 4 and 5 decompose 2x2x2 (6 neighbours): z faces packed
+    and sent through ncclSend / ncclRecv with real peers, axis-ordered 3-axis
+    deep halos (edges and corners ride the later phases), the overlapped
+    boundary onion and the lagged all-reduce — 8 processes on the one GPU,
+    eager replay (more than 4 ranks share the device: --stream-graphs auto
+    turns the per-stream graphs off).  Bitwise equal to the one-rank solve of
+    the same dtype, same stopping iteration.  Reference: heat3D.cu:243-263
+    (Cartesian topology), 619-641 / 724-755 (6-face exchange)."""
+    n, eps = 35, 1e-4
+    os.environ["LOCAL_WORLD_SIZE"] = "8"  # inherited by the spawned ranks: 8 processes share the GPU
+    try:
+        mp.start_processes(native_rccl_gpu_worker,
+                           args=(8, free_port(), str(tmp_path), n, eps, decomp, dtype, ["--watchdog", "60"]),
+                           nprocs=8, join=True, start_method="spawn")
+    finally:
+        del os.environ["LOCAL_WORLD_SIZE"]
+    single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="hip", device=0, dtype=dtype)
+    r1 = single.run()
+    it, err, name, graphs = open(tmp_path / "result.txt").read().split()
+    assert int(it) == r1["conv_iter"] and name == "rccl"
+    assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
+    meta = json.loads((tmp_path / "meta.json").read_text())
+    assert meta["dims"] == list(decomp) and meta["stream_graphs"] == "off", meta
+
+
+def test_bench_decomp_auto_times_candidates(gpu, tmp_path):
+    """``bench.py --gpus 4 --decomp auto``: every rank times each candidate
+    process grid (4x1x1 slabs, 2x2x1 blocks) through real RCCL at start-up,
+    the job keeps the fastest by its slowest rank, and the JSON lists every
+    candidate's ms/step (4 processes share the one GPU here, so the pick
+    itself says nothing about xGMI)."""
+    out = tmp_path / "d.json"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--comm", "rccl",
+                        "--rccl-host-split", "--grid", "96", "--steps", "6", "--warmup", "3",
+                        "--converge-eps", "0", "--profile-sweeps", "0", "--decomp-trial-steps", "12",
+                        "--timeout", "150", "--json-out", str(out)],
+                       capture_output=True, text=True, timeout=170, cwd=ROOT,
+                       env={k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")})
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = json.loads(out.read_text())
+    d = j["decomp_auto"]
+    assert [t["dims"] for t in d["trials"]] == [[4, 1, 1], [2, 2, 1]], d
+    assert all(t["ms_per_step"] > 0 for t in d["trials"])
+    best = min(d["trials"], key=lambda t: t["ms_per_step"])
+    assert d["dims"] in ([4, 1, 1], best["dims"])
+    assert j["placement"][0]["dims"] == d["dims"] and j["halo_verified"]
+    assert j["runtime"]["torch_loaded"] is False and "/opt/rocm" in j["runtime"]["hip_library"]

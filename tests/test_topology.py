@@ -113,3 +113,25 @@ def test_choose_dims_from_link_rate():
     assert choose_dims(N, 4, 10.0) == (4, 1, 1)
     assert choose_dims(N, 2, 1.0) == (2, 1, 1)
     assert choose_dims((40, 1024, 1024), 8, 10.0) == (2, 2, 2)   # slabs too thin: dims_create
+
+
+def test_decomp_candidates_and_measured_pick():
+    """bench.py --decomp auto: the candidate grids it times (slabs, 2D, 3D
+    blocks; only where every split axis keeps an interior between its K-deep
+    boundary layers) and the pick by the slowest rank's time, with a margin
+    that keeps the earlier (slab) candidate on a near tie."""
+    from heat3d_amd.parallel import decomp_candidates, pick_measured
+
+    assert decomp_candidates((1024,) * 3, 8) == [(8, 1, 1), (4, 2, 1), (2, 2, 2)]
+    assert decomp_candidates((1024,) * 3, 4) == [(4, 1, 1), (2, 2, 1)]
+    assert decomp_candidates((1024,) * 3, 2) == [(2, 1, 1)]
+    assert decomp_candidates((40, 40, 40), 8) == [(4, 2, 1), (2, 2, 2)]   # 38 / 8 < 7: no slabs
+    t = [{"dims": (8, 1, 1), "ms_per_step": 1.00}, {"dims": (4, 2, 1), "ms_per_step": 0.99},
+         {"dims": (2, 2, 2), "ms_per_step": 1.20}]
+    assert pick_measured(t) == (8, 1, 1)          # within the 2 % margin: slabs stay
+    t[1]["ms_per_step"] = 0.95
+    assert pick_measured(t) == (4, 2, 1)
+    t[2]["ms_per_step"] = 0.90
+    assert pick_measured(t) == (2, 2, 2)
+    with pytest.raises(ValueError):
+        pick_measured([{"dims": (2, 1, 1), "ms_per_step": None}])

@@ -25,6 +25,7 @@
 #   proxytrace [PROXY ARGS] the same under rocprofv3 --kernel-trace          -> OUT/proxytrace<i>/
 #   pmc VARIANT [N] [DTYPE] tools/pmc_passes.sh (one counter group per run) -> OUT/pmc<i>/
 #   py SCRIPT [ARGS]        any python script                              -> OUT/py<i>.log
+#   exe BINARY [ARGS]       a probe binary, 120 s limit                     -> OUT/exe<i>.log
 #   sh COMMAND...           a shell command (keep GPU work under its own timeout)
 #   env VAR=VALUE ...       export for the later steps
 set -o pipefail
@@ -114,6 +115,9 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python3 -u "${args[@]}" > "$OUT/py$i.log" 2>&1 || { rc=$?; tail -20 "$OUT/py$i.log"; fail py $rc; }
       tail -20 "$OUT/py$i.log" ;;
+    exe)
+      timeout -k 5 120 "${args[@]}" > "$OUT/exe$i.log" 2>&1 || { rc=$?; tail -20 "$OUT/exe$i.log"; fail exe $rc; }
+      tail -30 "$OUT/exe$i.log" ;;
     sh)
       bash -c "${args[*]}" || fail sh $? ;;
     env)

@@ -63,6 +63,12 @@ static int run_case(Ctx& c, int which, bool consumer_first) {
   hipEvent_t e1, e2;
   CK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
   CK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+  // both events recorded (complete) before the captures: the first probe
+  // build, whose case 3 captured a wait on a never-recorded event, crashed
+  // the HIP 7.2 runtime (SIGSEGV) in that capture
+  CK(hipEventRecord(e1, c.s1));
+  CK(hipEventRecord(e2, c.s1));
+  CK(hipStreamSynchronize(c.s1));
   hipGraph_t ga, gb, tmp;
   CK(hipGraphCreate(&ga, 0));
   CK(hipGraphCreate(&gb, 0));
@@ -154,6 +160,7 @@ int main() {
   CK(hipStreamCreateWithFlags(&c.s2, hipStreamNonBlocking));
   CK(hipMalloc(&c.tick, 4));
   CK(hipMalloc(&c.slots, 16));
+  std::printf("(%s)\n", "tickets: a0 / a1 = graph A, b = graph B; -1 = not in this case");
   int rc = run_case(c, 1, false);
   if (!rc) rc = run_case(c, 1, true);
   if (!rc) rc = run_case(c, 2, false);
