@@ -65,7 +65,9 @@ class PhantomComm final : public Comm {
       // interior sweep whether it keeps four or eight 16-byte loads in flight
       // per lane (8 groups per 64 GB/s transfer ran the wire 2x long,
       // gpurun_out/r7x; 16 ran it 9-17 % long, r7m)
-      const int per = std::max(channels_, (int)std::ceil(gbps_ / 2.0));
+      // (at most 64, the copy kernel's limit: faster emulated links keep 64
+      // groups, each then streaming more than ~2 GB/s)
+      const int per = std::min(64, std::max(channels_, (int)std::ceil(gbps_ / 2.0)));
       std::vector<hip::PacedCopy> pc;
       for (const auto& x : xs) {
         if (x.dst_rank != rank_ || x.src_rank == rank_) continue;

@@ -130,7 +130,7 @@ std::string Config::usage() {
      << "  --no-rccl-graph           never record RCCL calls into hipGraphs (eager multi-rank steps)\n"
      << "  --rccl-shared             one RCCL communicator for halos and all-reduces\n"
      << "  --rccl-p2p-channels N     RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS unless set in the\n"
-     << "                            environment): 0 auto = the reserved CUs (8), -1 RCCL's default\n"
+     << "                            environment): N > 0 that many; default RCCL's own\n"
      << "  --mem-reserve-gb G        memory preflight reserve (default 2)\n"
      << "  --no-mem-preflight        skip the memory preflight\n"
      << "  --host-mem-limit-gb G     host RAM budget of the gather-to-root Tecplot (default RAM/2)\n"

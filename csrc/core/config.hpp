@@ -96,7 +96,7 @@ struct Config {
   double graph_canary_s = 2.0;    // device-wait timeout of the canary replay (0: no canary)
   bool rccl_graph = true;         // RCCL calls may be recorded into hipGraphs (tests/test_gpu_rccl.py)
   bool rccl_shared = false;       // one RCCL communicator for halos and all-reduces (else ncclCommSplit)
-  int rccl_p2p_channels = 0;      // RCCL P2P channel pool: 0 auto (the reserved CUs, 8), -1 RCCL's default
+  int rccl_p2p_channels = 0;      // RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS): N > 0 that many, else RCCL's default
   double mem_reserve_gb = 2.0;    // memory preflight: reserve for RCCL, code objects, scratch
   bool mem_preflight = true;      // refuse configurations that do not fit before allocating
   double host_mem_limit_gb = 0;   // gather-to-root Tecplot: host RAM budget (0 = half of RAM)

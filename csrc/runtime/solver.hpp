@@ -313,8 +313,8 @@ class Solver {
   std::vector<Local> local_;
   bool has_halo_ = false;  // any face with a neighbour on any local subdomain
   bool overlap_ = true;
-  bool tb_overlap_ = false;
-  bool long_slab_ = false;    // x-slab share whose interior hides the halo chain (no CU reservation)   // sweeps: interior || (deep halo -> boundary slabs)
+  bool tb_overlap_ = false;   // sweeps: interior || (deep halo -> boundary slabs)
+  bool long_slab_ = false;    // x-slab share whose interior hides the halo chain (no CU reservation)
   int64_t hd_[3] = {1, 1, 1}; // ghost depth per axis (K on split axes with temporal blocking, K+1 with long_halo_)
   int64_t xd_[3] = {1, 1, 1}; // regular exchange depth per axis (K on split axes with temporal blocking)
   // Long sweeps (depth K+1) across halos: ghosts allocated K+1 deep on split
@@ -352,8 +352,8 @@ class Solver {
   std::size_t planned_bytes_ = 0, mem_free_before_ = 0, mem_total_ = 0;
   void preflight_memory();
   bool lag_ = false;
-  int64_t nsweep_ = 0;
-  double fake_allreduce_us_ = 0;  // diagnostic: emulated all-reduce latency (virtual ranks)        // overlapped sweeps issued (event / residual-slot parity)
+  int64_t nsweep_ = 0;            // overlapped sweeps issued (event / residual-slot parity)
+  double fake_allreduce_us_ = 0;  // diagnostic: emulated all-reduce latency (virtual ranks)
   bool tb_ = false;           // K-step temporal blocking active
   int K_ = 1;                 // iterations per sweep
   KernelSpec kspec2_;
@@ -423,10 +423,11 @@ inline RcclOptions rccl_options(const Config& c) {
   RcclOptions o;
   o.shared = c.rccl_shared;
   o.graph = c.rccl_graph;
-  // the P2P kernels' blocks fit the CUs the compute stream leaves free
-  o.p2p_channels = c.rccl_p2p_channels > 0    ? c.rccl_p2p_channels
-                   : c.rccl_p2p_channels == 0 ? (c.reserve_cus > 0 ? c.reserve_cus : 8)
-                                              : 0;
+  // RCCL's P2P channel pool: its default unless asked for.  (Round 5 capped
+  // it at the reserved CUs for every RCCL job, before the communicator knew
+  // the reservation the solver would choose, and never timed the cap on real
+  // xGMI links: opt-in until a multi-GPU A/B shows it does not cost halo rate.)
+  o.p2p_channels = c.rccl_p2p_channels > 0 ? c.rccl_p2p_channels : 0;
   return o;
 }
 inline PhantomOptions phantom_options(const Config& c) {
