@@ -127,6 +127,8 @@ std::string Config::usage() {
      << "  --graph-canary S          device-wait timeout of the start-up canary replay of those graphs; a\n"
      << "                            rank whose replay times out or runs > 2x eager turns them off for the\n"
      << "                            job (default 2; 0 = no canary)\n"
+     << "  --no-fused-check          single-subdomain sweeps: a check kernel after each sweep instead of\n"
+     << "                            the check in the sweep's last workgroup\n"
      << "  --no-rccl-graph           never record RCCL calls into hipGraphs (eager multi-rank steps)\n"
      << "  --rccl-shared             one RCCL communicator for halos and all-reduces\n"
      << "  --rccl-p2p-channels N     RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS unless set in the\n"
@@ -279,6 +281,7 @@ Config Config::parse(int argc, const char* const* argv) {
       c.stream_graphs = v == "auto" ? -1 : v == "on" ? 1 : 0;
     }
     else if (key == "--graph-canary") c.graph_canary_s = to_f64(get("--graph-canary"), "--graph-canary");
+    else if (key == "--no-fused-check") c.fuse_check = false;
     else if (key == "--rccl-graph") c.rccl_graph = true;
     else if (key == "--no-rccl-graph") c.rccl_graph = false;
     else if (key == "--rccl-shared") c.rccl_shared = true;

@@ -94,6 +94,9 @@ struct Config {
   // rank turns them off for the job (Solver::canary_stream_graphs).
   int stream_graphs = -1;
   double graph_canary_s = 2.0;    // device-wait timeout of the canary replay (0: no canary)
+  // single-subdomain K-step sweeps run their convergence check in the sweep's
+  // last workgroup (StencilParams::fuse_check) instead of a kernel after it
+  bool fuse_check = true;
   bool rccl_graph = true;         // RCCL calls may be recorded into hipGraphs (tests/test_gpu_rccl.py)
   bool rccl_shared = false;       // one RCCL communicator for halos and all-reduces (else ncclCommSplit)
   int rccl_p2p_channels = 0;      // RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS): N > 0 that many, else RCCL's default

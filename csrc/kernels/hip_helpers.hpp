@@ -122,6 +122,33 @@ __device__ __forceinline__ void residual_commit(unsigned long long* slot, double
   if ((threadIdx.x & 63) == 0) slot_max(slot, b);
 }
 
+// Fused convergence check of a K-step sweep (StencilParams::fuse_check), run
+// by every workgroup after its residual commit (or instead of it, when the
+// sweep is a no-op because the run has converged): each workgroup takes a
+// ticket once its residual atomics are visible (release, agent scope); the
+// one that draws the last ticket (acquire) sees every workgroup's slot_max,
+// runs check_convergence over the K slots in order, resets them and the
+// ticket counter — what check_kernel did after the sweep.  Every thread of
+// the workgroup must reach it (barrier).
+template <int K>
+__device__ __forceinline__ void fused_check_tail(DeviceState* st, int slot, int nblocks) {
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  const unsigned t = __hip_atomic_fetch_add(&st->sweep_tickets, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (t != (unsigned)nblocks - 1u) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    unsigned long long* rs = &st->residual[slot + i];
+    const unsigned long long bits = __hip_atomic_load(rs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    check_convergence_scalar(st, __builtin_bit_cast(double, (long long)bits));
+    __hip_atomic_store(rs, kResidualInitBits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __hip_atomic_store(&st->sweep_tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+}
+
 // Workgroup-level commit of K residual slots: one wave max per slot into LDS,
 // then lanes s < K of wave 0 reduce over the NW waves and commit once.  Must
 // be reached by every thread of the workgroup (contains a barrier).

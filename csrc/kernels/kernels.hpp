@@ -67,6 +67,12 @@ struct StencilParams {
   // false: the kernel honours state->done (a no-op once converged) but
   // records no residual (Solver::preheat's idempotent warm-up sweeps)
   bool residual = true;
+  // K-step sweeps of a single-subdomain run: the last workgroup to finish runs
+  // the convergence check of the sweep's K residual slots (check_convergence
+  // semantics, bitwise the same state) instead of a separate check kernel
+  // after it, which cost ~10 us per sweep on the critical path (a one-lane
+  // kernel and its dispatch; profiles/r06)
+  bool fuse_check = false;
 };
 
 struct InitParams {

@@ -80,6 +80,11 @@ struct DeviceState {
   // device-side cross-stream waits of per-stream hipGraphs give up after this
   // many 100 MHz ticks (read at every wait: the start-up canary shortens it)
   uint64_t wait_ticks;
+  // sweeps with a fused convergence check (StencilParams::fuse_check): the
+  // workgroups that finished the current sweep; the last one runs the check
+  // and resets it to 0
+  uint32_t sweep_tickets;
+  uint32_t pad0;
   int64_t hist_cap;                // residual history ring capacity
   double hist[1024];               // residual history ring (index = iter % cap)
 };

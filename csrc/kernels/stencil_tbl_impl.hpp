@@ -63,6 +63,8 @@ struct TBLArgs {
   int nzb, nyb;
   int segsplit, n1, rb;        // x plan: seg | split << 16, whole pieces, r | split-tail << 30
   int zs;                      // tile stride along z = stored columns per tile (<= 64 - 2K)
+  DeviceState* fst;            // fused convergence check (fused_check_tail): state, nullptr = off
+  int fslot, fblocks;          // its first residual slot and the grid's workgroup count
 };
 
 namespace {
@@ -125,7 +127,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
   static_assert(YS > 0 && R <= 16, "tile too small for depth K");
   __shared__ __attribute__((aligned(16))) Real s_row[2][K][WY][2][64];
   static_assert(sizeof(s_row) >= WY * K * sizeof(unsigned long long), "residual scratch");
-  if (flag_set(done)) return;
+  if (flag_set(done)) {
+    if (g.fst) fused_check_tail<K>(g.fst, g.fslot, g.fblocks);
+    return;
+  }
 
   // piece decode: blocks dealt round-robin over the 8 XCDs; consecutive
   // pieces (neighbouring tiles) share an XCD's L2 (same encoding as tbr)
@@ -358,6 +363,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     residual_commit_block<WY, K>(res, mm, nan_seen,
                                  *reinterpret_cast<unsigned long long(*)[WY][K]>(&s_row[0][0][0][0][0]));
   }
+  if (g.fst) fused_check_tail<K>(g.fst, g.fslot, g.fblocks);
 }
 
 template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>
@@ -383,7 +389,7 @@ void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
   HEAT3D_CHECK(Ln0 + 2 * Lg0 < (1LL << 30) && Ln1 + 2 * Lg1 < (1LL << 30) &&
                    Lsy * (int64_t)sizeof(Real) * (R + 2 * Lg1 + TY + 2 * K) < (1LL << 31),
                "tl: extents exceed 32-bit tile coordinates");
-  TBLArgs g;
+  TBLArgs g{};
   g.sx = Lsx;
   g.sy = Lsy;
   g.origin = L.origin;
@@ -451,6 +457,9 @@ void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
     ga.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
     const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
     HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl: bad block count " << nblocks);
+    ga.fst = p.fuse_check && r ? p.state : nullptr;
+    ga.fslot = p.slot;
+    ga.fblocks = (int)nblocks;
     if (trace_enabled())
       std::fprintf(stderr, "[heat3d trace] tl K=%d box x %lld: zs=%d L=%d seg=%d tiles=%dx%d blocks=%lld (model %.1f)\n",
                    K, (long long)nxb, zs, Lx, xp.seg, ga.nzb, ga.nyb, (long long)nblocks,

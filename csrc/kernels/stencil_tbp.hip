@@ -67,6 +67,8 @@ struct TBPArgs {
   int segsplit, n1, rb;        // x plan (TBRArgs encoding)
   int hl;                      // first stored column of a tile, from its first loaded one
   int zs;                      // tile stride along z = stored columns per tile (even, <= 128 - 2K - 2)
+  DeviceState* fst;            // fused convergence check (fused_check_tail): state, nullptr = off
+  int fslot, fblocks;          // its first residual slot and the grid's workgroup count
 };
 
 namespace {
@@ -147,7 +149,10 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const T* __restrict__ in,
   static_assert(YS > 0 && R <= 16, "tile too small for depth K");
   __shared__ __attribute__((aligned(16))) f2 s_row[2][K][WY][2][64];
   static_assert(sizeof(s_row) >= WY * K * sizeof(unsigned long long), "residual scratch");
-  if (flag_set(done)) return;
+  if (flag_set(done)) {
+    if (g.fst) fused_check_tail<K>(g.fst, g.fslot, g.fblocks);
+    return;
+  }
 
   auto remap = [](int i, int n) {
     const int c = i & 7;
@@ -350,6 +355,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const T* __restrict__ in,
     residual_commit_block<WY, K>(res, mm, nan_seen,
                                  *reinterpret_cast<unsigned long long(*)[WY][K]>(&s_row[0][0][0][0][0]));
   }
+  if (g.fst) fused_check_tail<K>(g.fst, g.fslot, g.fblocks);
 }
 
 // Tile stride along z: 128 - 2K - 2 stored columns (tiles start on even
@@ -403,7 +409,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
   HEAT3D_CHECK(L.n[0] + 2 * L.gx < (1LL << 30) && L.n[1] + 2 * L.gy < (1LL << 30) &&
                    L.sy * (int64_t)sizeof(T) * (R + 2 * L.gy + TY + 2 * K) < (1LL << 31),
                "tl pair: extents exceed 32-bit tile coordinates");
-  TBPArgs g;
+  TBPArgs g{};
   g.sx = L.sx;
   g.sy = L.sy;
   g.origin = L.origin;
@@ -474,6 +480,9 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
     ga.rb = xp.r | (xp.nb2 > 0 ? (1 << 30) : 0);
     const int64_t nblocks = (int64_t)xp.n1 + xp.r + xp.nb2;
     HEAT3D_CHECK(nblocks < (1LL << 31) && nblocks >= 1, "tl pair: bad block count " << nblocks);
+    ga.fst = p.fuse_check && r ? p.state : nullptr;
+    ga.fslot = p.slot;
+    ga.fblocks = (int)nblocks;
     if (trace_enabled())
       std::fprintf(stderr,
                    "[heat3d trace] tl pair K=%d box x %lld: zs=%d L=%d seg=%d tiles=%dx%d blocks=%lld slots=%d "

@@ -1256,11 +1256,18 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
     if (has_halo_) enqueue_halo(bi, kCompute, dv);
     be_->range_push("sweep");
     prof_record(prof_idx_, PE_INT0, kCompute);
-    for (auto& l : local_) be_->sweep(dt_, params(l, dv ? l.tb_interior_long : l.tb_interior), ks, kCompute);
+    // one subdomain, nothing to all-reduce: the sweep's last workgroup runs
+    // the check (no check kernel and its dispatch on the critical path)
+    const bool fused = fused_check();
+    for (auto& l : local_) {
+      StencilParams sp = params(l, dv ? l.tb_interior_long : l.tb_interior);
+      sp.fuse_check = fused;
+      be_->sweep(dt_, sp, ks, kCompute);
+    }
     prof_record(prof_idx_, PE_INT1, kCompute);
     be_->range_pop();
     prof_record(prof_idx_, PE_RED0, kCompute);
-    reduce_and_check(kCompute, slot0, Kp, prof_idx_);
+    if (!fused) reduce_and_check(kCompute, slot0, Kp, prof_idx_);
     prof_record(prof_idx_, PE_CHK1, kCompute);
     if (!capturing_) {
       for (int i = 0; i < 2; ++i) {
@@ -1339,6 +1346,11 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   pending_.prof = prof_idx_;
   if (!chain_) flush_pending_reduce();
   ++nsweep_;
+}
+
+bool Solver::fused_check() const {
+  return cfg_.fuse_check && be_->is_gpu() && tb_ && !tb_overlap_ && local_.size() == 1 &&
+         (comm_->all_local() || comm_->size() == 1) && fake_allreduce_us_ <= 0;
 }
 
 void Solver::reduce_and_check(StreamId s, int slot0, int Kp, int prof) {

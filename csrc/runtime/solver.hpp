@@ -273,6 +273,9 @@ class Solver {
   void comm_token_signal(StreamId s);
   // all-reduce + check of one sweep (residual slots slot0 .. slot0+Kp-1)
   void reduce_and_check(StreamId s, int slot0, int Kp, int prof = -1);
+  // the non-overlapped sweep of a single-subdomain run checks convergence in
+  // its last workgroup (StencilParams::fuse_check; --no-fused-check: off)
+  bool fused_check() const;
   // lagged overlapped sweeps: the all-reduce of sweep q is issued after the
   // halo of sweep q+1 (see enqueue_multi); flush issues a pending one
   void flush_pending_reduce();

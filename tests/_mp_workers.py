@@ -124,15 +124,27 @@ def native_rccl_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, ext
     all-reduce of the residual slots through the production schedule."""
     os.environ.update({"NCCL_HOSTID": f"heat3d-test-rank{rank}", "NCCL_SOCKET_IFNAME": "lo"})
     dist = _init(rank, world, port)
+    import time
+
     import heat3d_amd
+
+    t0 = time.perf_counter()
+
+    def stage(what):  # progress on stderr (pytest -s shows it; a hang names its stage)
+        print(f"[rccl worker {rank}/{world} {time.perf_counter() - t0:7.2f} s] {what}", file=sys.stderr, flush=True)
 
     s = heat3d_amd.HeatSolver((n, n, n), 10 ** 6, eps, backend="hip", comm="rccl", decomp=decomp,
                               dtype=dtype, device=0, extra_args=list(extra_args))
+    stage("communicator up")
     assert s.native.comm_name.startswith("rccl"), s.native.comm_name
     assert s.native.comm_transport_ranks == world
+    s.initialize()
+    stage(f"initialized (stream graphs {s.native.stream_graphs_state})")
     r = s.run()
+    stage(f"converged at {r['conv_iter']}")
     assert s.native.verify_halos() == 0  # checksums exchanged over RCCL
     g = s.gather()  # ncclSend / ncclRecv of every rank's block to rank 0
+    stage("gathered")
     if rank == 0:
         np.save(os.path.join(outdir, "field.npy"), g)
         with open(os.path.join(outdir, "result.txt"), "w") as f:

@@ -153,9 +153,11 @@ def test_rccl_8rank_blocks_bitwise(h3d, gpu, tmp_path, decomp, dtype):
     boundary onion and the lagged all-reduce — 8 processes on the one GPU,
     eager replay (more than 4 ranks share the device: --stream-graphs auto
     turns the per-stream graphs off).  Bitwise equal to the one-rank solve of
-    the same dtype, same stopping iteration.  Reference: heat3D.cu:243-263
+    the same dtype, same stopping iteration.  eps 1e-2 (188 iterations): 8
+    ranks on one GPU over RCCL's loopback network transport take ~80 ms per
+    step (profiles/r06/rccl8_2x2x2_rehearsal.json).  Reference: heat3D.cu:243-263
     (Cartesian topology), 619-641 / 724-755 (6-face exchange)."""
-    n, eps = 35, 1e-4
+    n, eps = 35, 1e-2
     os.environ["LOCAL_WORLD_SIZE"] = "8"  # inherited by the spawned ranks: 8 processes share the GPU
     try:
         mp.start_processes(native_rccl_gpu_worker,

@@ -196,3 +196,29 @@ def test_schedule_autotune_bitwise(h3d, gpu, vr):
     for t in mine:
         assert t["candidates"] >= 2 and t["ms"] > 0 and t["ms"] <= t["ms_model"] + 1e-9, t
         assert t["L"] == -3 or t["L"] > 0, t
+
+
+@pytest.mark.parametrize("n,eps,kernel2,dtype", [((33, 33, 33), 1e-5, "auto", "fp64"),
+                                                 ((65, 47, 130), 1e-4, "tl3:2", "fp64"),
+                                                 ((64, 64, 64), 1e-4, "auto", "fp32"),
+                                                 ((40, 40, 40), 1e-3, "tl4", "fp64")])
+def test_fused_check_bitwise(h3d, gpu, n, eps, kernel2, dtype):
+    """Single-subdomain sweeps check convergence in their last workgroup
+    (StencilParams::fuse_check) instead of a check kernel after them: the same
+    stopping iteration, residual history and field, bit for bit, as the
+    separate check (--no-fused-check); also a converged run's remaining
+    sweeps (no-ops whose workgroups still take their tickets) keep counting."""
+    kw = dict(backend="hip", dtype=dtype, extra_args=["--kernel2", kernel2])
+    a = h3d.HeatSolver(n, 10 ** 6, eps, **kw)
+    b = h3d.HeatSolver(n, 10 ** 6, eps, **dict(kw, extra_args=kw["extra_args"] + ["--no-fused-check"]))
+    ra, rb = a.run(), b.run()
+    assert ra["converged"] and ra["conv_iter"] == rb["conv_iter"], (ra, rb)
+    assert ra["last_residual"] == rb["last_residual"] and ra["norm"] == rb["norm"]
+    assert np.array_equal(a.gather(), b.gather())
+    # past convergence: a fixed number of (no-op) sweeps still advances the check count
+    for s in (a, b):
+        s.initialize()
+        s.step(30)
+        s.synchronize()
+    sa, sb = a.state(), b.state()
+    assert sa["iter"] == sb["iter"] == 30 and sa["fault"] == sb["fault"] == 0, (sa, sb)

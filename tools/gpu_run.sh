@@ -47,7 +47,7 @@ rccl_ranks() {  # $1 = n, $2 = tag, $3 = 1 to trace, rest = bench args
     [ "$trace" = 1 ] && pre=(rocprofv3 --kernel-trace --output-format csv -d "$OUT/$tag/rank$r" -o trace --)
     RANK=$r LOCAL_RANK=$r WORLD_SIZE=$n LOCAL_WORLD_SIZE=$n GROUP_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=$port \
       NCCL_HOSTID=heat3d-run-rank$r NCCL_SOCKET_IFNAME=lo \
-      timeout -k 10 400 "${pre[@]}" python3 -u bench.py --gpus "$n" --comm rccl --watchdog 120 "$@" \
+      timeout -k 10 "${RANK_TIMEOUT:-400}" "${pre[@]}" python3 -u bench.py --gpus "$n" --comm rccl --watchdog 120 "$@" \
       > "$OUT/$tag.rank$r.log" 2>&1 &
     pids+=($!)
   done
