@@ -116,6 +116,8 @@ def parse_args(argv=None):
                          "seconds (0 disables)")
     ap.add_argument("--verbose", type=int, default=0,
                     help="time-to-converge run: print the residual every N iterations (stdout, rank 0)")
+    ap.add_argument("--solver-flags", default="",
+                    help="extra native solver flags for A/B runs, e.g. \"--no-fused-check --lag off\"")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -243,7 +245,7 @@ def run_rank(args) -> int:
                           extra_args=["--stream-graphs", args.stream_graphs, "--graph-canary", str(args.graph_canary),
                                       "--temporal", str(args.temporal), "--kernel2", args.kernel2,
                                       "--watchdog", str(args.watchdog), "--reserve-cus", str(args.reserve_cus)]
-                          + list(extra))
+                          + args.solver_flags.split() + list(extra))
 
     if trials is not None:
         # --decomp auto: time each candidate process grid (x slabs, 2D, 3D
@@ -414,6 +416,7 @@ def run_rank(args) -> int:
                    "ranks_per_device": per_dev,
                    "graph_launches": graph_launches,
                    "overlap": not args.no_overlap, "comm": comm_name, "reserved_cus": reserved,
+                   "solver_flags": args.solver_flags or None,
                    "preheat_sweeps": preheat},
         "comm_ranks": comm_ranks,
         # --decomp auto: every candidate grid's timed ms/step (slowest rank)
