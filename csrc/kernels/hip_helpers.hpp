@@ -206,7 +206,10 @@ int device_cus();
 // 122 x 1022^2, runs 774 GLUPS with 56-column tiles against 723 with 58;
 // profiles/xplan_calibration_r03.md).  tune_schedule times, twice each, every
 // (z stride, spec field L) candidate on `s` — per stride in zs_opts the
-// model's x plan (L = -3) and fixed segments of nx/k planes — keeps the
+// model's x plan (L = -3), fixed segments of nx/k planes and (round 6, with
+// nyb > 0: the y tile count, so that the tiles of each stride are known) the
+// model's best fixed segment lengths of any size, whose last piece per tile
+// is short — keeps the
 // fastest (the model's choice, candidate 0, unless another is >= 1.5% faster
 // in a confirming interleaved rerun) per (device, kernel, box, slots,
 // reserved CUs) and returns it; tuned_lookup returns a kept choice.
@@ -216,7 +219,8 @@ struct SchedChoice {
 bool tuned_lookup(const void* kfn, const int64_t box[3], int slots, int reserved, SchedChoice* out);
 SchedChoice tune_schedule(const char* name, const void* kfn, const int64_t box[3], int slots, int reserved, int U,
                           const std::vector<int>& zs_opts, hipStream_t s,
-                          const std::function<void(int, int)>& launch);
+                          const std::function<void(int, int)>& launch, int64_t nyb = 0, int fill = 0);
+
 
 }  // namespace hip
 }  // namespace heat3d

@@ -109,6 +109,13 @@ struct XPlanInfo {
   double makespan = 0;
 };
 XPlanInfo describe_xplan(int64_t nx, int64_t tiles, int slots, int fill, int U, int seg);
+// The `count` fixed x-segment lengths (>= U planes, any length: a tile's last
+// piece may be short) with the smallest modelled makespan for `tiles` tiles of
+// nx planes on `slots` workgroups, best first.  Equal segments (nx / k) leave
+// slots idle or add a round when tiles x k is just above a multiple of the
+// slots; e.g. 1022^3 fp32 pairs (225 tiles): 918-plane segments model 932
+// plane-steps per slot against the x plan's 1024 (ideal 902).
+std::vector<int> best_fixed_segments(int64_t nx, int64_t tiles, int slots, int fill, int U, int count);
 
 // sweep schedules chosen by timing (StencilParams::tune): kernel, box, the
 // winning z tile stride and spec-field-L value (-3 = the model's x plan, > 0

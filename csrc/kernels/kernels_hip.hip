@@ -361,6 +361,38 @@ double tiling_cost(const XPlan& p, int64_t nx, int64_t tiles, int slots, int fil
   return std::max(xplan_makespan(p, nx, tiles, slots, fill, U), work);
 }
 
+std::vector<int> best_fixed_segments(int64_t nx, int64_t tiles, int slots, int fill, int U, int count) {
+  std::vector<std::pair<double, int>> ms;
+  std::vector<double> heap;
+  if (nx < 2 * U || tiles < 1 || count < 1) return {};
+  // a coarse grid of lengths (<= ~256 of them), then every length around the
+  // best few: the makespan is piecewise smooth in the segment length
+  const int lo = std::max<int>(U, (int)(nx / 32));
+  const int step = std::max<int>(1, (int)((nx - lo) / 256));
+  auto eval = [&](int seg) {
+    for (const auto& m : ms)
+      if (m.second == seg) return;
+    ms.push_back({simulate_xplan(fixed_xplan(nx, tiles, seg), nx, tiles, slots, fill, U, heap), seg});
+  };
+  for (int seg = lo; seg <= (int)nx; seg += step) eval(seg);
+  std::sort(ms.begin(), ms.end());
+  std::vector<int> coarse;
+  for (std::size_t i = 0; i < ms.size() && i < 3; ++i) coarse.push_back(ms[i].second);
+  for (int c : coarse)
+    for (int seg = std::max(lo, c - step); seg <= std::min<int>((int)nx, c + step); ++seg) eval(seg);
+  std::sort(ms.begin(), ms.end());
+  std::vector<int> out;
+  for (const auto& m : ms) {
+    if ((int)out.size() >= count) break;
+    // distinct pieces: lengths giving the same segment count and makespan
+    // within a chunk of each other add nothing to time
+    bool near = false;
+    for (int o : out) near |= std::abs(o - m.second) < U;
+    if (!near) out.push_back(m.second);
+  }
+  return out;
+}
+
 XPlan plan_x(int64_t nx, int64_t tiles, int slots, int fill, int U, bool equal_only) {
   struct Key {
     int64_t nx, tiles;
@@ -443,7 +475,7 @@ bool tuned_lookup(const void* kfn, const int64_t box[3], int slots, int reserved
 
 SchedChoice tune_schedule(const char* name, const void* kfn, const int64_t box[3], int slots, int reserved, int U,
                           const std::vector<int>& zs_opts, hipStream_t s,
-                          const std::function<void(int, int)>& launch) {
+                          const std::function<void(int, int)>& launch, int64_t nyb, int fill) {
   int dev = 0;
   HIPK_CHECK(hipGetDevice(&dev));
   const TuneKey key{dev, kfn, box[0], box[1], box[2], slots, reserved};
@@ -471,6 +503,14 @@ SchedChoice tune_schedule(const char* name, const void* kfn, const int64_t box[3
       if (seg < U || seg >= (1 << 15) || std::find(segs.begin(), segs.end(), seg) != segs.end()) continue;
       segs.push_back(seg);
       cand.push_back({zs, seg});
+    }
+    if (nyb > 0) {
+      const int64_t tiles = std::max<int64_t>(1, (box[2] + zs - 1) / zs) * nyb;
+      for (int seg : best_fixed_segments(nx, tiles, slots, fill, U, 2)) {
+        if (seg >= (1 << 15) || std::find(segs.begin(), segs.end(), seg) != segs.end()) continue;
+        segs.push_back(seg);
+        cand.push_back({zs, seg});
+      }
     }
   }
   struct Ev {  // released on every exit, a throwing launch included

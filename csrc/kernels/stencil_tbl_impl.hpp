@@ -477,7 +477,8 @@ void launch_tbl(const StencilParams& p, const KernelSpec& ks, hipStream_t s) {
       const int wide = 64 - 2 * K, aligned = sizeof(Real) == 8 ? wide & ~7 : wide;
       for (int z : {wide, aligned})
         if (std::find(zs_opts.begin(), zs_opts.end(), z) == zs_opts.end()) zs_opts.push_back(z);
-      tune_schedule(sizeof(Real) == 8 ? "tl-fp64" : "tl-fp32", kfn, box, slots, p.cu_reserved, U, zs_opts, s, fire);
+      tune_schedule(sizeof(Real) == 8 ? "tl-fp64" : "tl-fp32", kfn, box, slots, p.cu_reserved, U, zs_opts, s, fire,
+                    g.nyb, 2 * (K - 1));
       return;  // every candidate computed this sweep
     }
     SchedChoice c;

@@ -503,7 +503,7 @@ static void launch_tbp(const StencilParams& p, const KernelSpec& ks, hipStream_t
       for (int z : {wide, aligned})
         if (z > 0 && std::find(zs_opts.begin(), zs_opts.end(), z) == zs_opts.end()) zs_opts.push_back(z);
       tune_schedule(sizeof(T) == 8 ? "tl-fp64-pair" : "tl-fp32-pair", kfn, box, slots, p.cu_reserved, U, zs_opts, s,
-                    fire);
+                    fire, g.nyb, 2 * (K - 1));
       return;
     }
     SchedChoice c;

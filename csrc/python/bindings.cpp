@@ -186,6 +186,9 @@ PYBIND11_MODULE(_heat3d, m) {
     d["ideal"] = (double)tiles * (double)(nx + fill) / slots;
     return d;
   }, py::arg("nx"), py::arg("tiles"), py::arg("slots"), py::arg("fill"), py::arg("U"), py::arg("seg") = 0);
+  // the start-up tuner's model-best fixed x segments (any length)
+  m.def("best_fixed_segments", &heat3d::hip::best_fixed_segments, py::arg("nx"), py::arg("tiles"), py::arg("slots"),
+        py::arg("fill"), py::arg("U"), py::arg("count") = 2);
   // x schedules chosen by timing at solver start-up (Config::autotune)
   m.def("tuned_schedules", []() {
     py::list out;

@@ -469,3 +469,21 @@ def test_long_sweep_across_halos_rollback(h3d, vr, dims):
             r = s.run()
             assert r["converged"] and r["conv_iter"] == c, (eps, j, r, c)
             assert np.array_equal(s.gather(), ref.gather()), (vr, eps, j)
+
+
+def test_best_fixed_segments_beat_the_plan_model():
+    """The start-up tuner's extra x-schedule candidates (round 6): fixed
+    segments of any length, whose last piece per tile is short.  In the
+    dispatch model they beat the x plan where its equal pieces leave a round
+    part-empty (1022^3 fp32 pairs: 225 tiles; 510^3 fp64: 117 tiles), and are
+    never worse than the best equal split."""
+    import heat3d_amd
+
+    e = heat3d_amd.native()
+    for nx, tiles, want in ((1022, 225, 0.92), (510, 117, 0.95), (1022, 475, 0.96), (2046, 882, 1.0)):
+        segs = e.best_fixed_segments(nx, tiles, 256, 4, 6, 2)
+        assert len(segs) == 2 and all(6 <= s <= nx for s in segs), segs
+        best = e.x_plan(nx, tiles, 256, 4, 6, segs[0])["makespan"]
+        plan = e.x_plan(nx, tiles, 256, 4, 6, 0)["makespan"]
+        equal = min(e.x_plan(nx, tiles, 256, 4, 6, -(-nx // k))["makespan"] for k in range(1, 17))
+        assert best <= want * plan and best <= equal, (nx, tiles, segs, best, plan, equal)
