@@ -125,28 +125,34 @@ __device__ __forceinline__ void residual_commit(unsigned long long* slot, double
 // Fused convergence check of a K-step sweep (StencilParams::fuse_check), run
 // by every workgroup after its residual commit (or instead of it, when the
 // sweep is a no-op because the run has converged): each workgroup takes a
-// ticket once its residual atomics are visible (release, agent scope); the
-// one that draws the last ticket (acquire) sees every workgroup's slot_max,
-// runs check_convergence over the K slots in order, resets them and the
-// ticket counter — what check_kernel did after the sweep.  Every thread of
-// the workgroup must reach it (barrier).
+// ticket once its residual atomics are acknowledged; the one that draws the
+// last ticket swaps the K slots back to their initial value (an atomic
+// exchange returns the value at the atomics' coherence point, whatever this
+// XCD's L2 holds), runs check_convergence over them in order and resets the
+// ticket counter —
+// what check_kernel did after the sweep.  No agent-scope fences: a release
+// fence is an L2 write-back (buffer_wbl2), which every one of the sweep's
+// ~2000 workgroups issuing it cost 6-7 % of the 1022^3 sweep (round 6,
+// gpurun_out/r6e); only the residual atomics must be ordered before the
+// ticket (s_waitcnt), the state fields the last workgroup writes are read by
+// later kernels and the host, after this kernel's end-of-kernel release.
+// Every thread of the workgroup must reach it (barrier).
 template <int K>
 __device__ __forceinline__ void fused_check_tail(DeviceState* st, int slot, int nblocks) {
   __syncthreads();
   if (threadIdx.x != 0) return;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  const unsigned t = __hip_atomic_fetch_add(&st->sweep_tickets, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's residual atomics (wave 0 issued them) acknowledged
+  const unsigned t = __hip_atomic_fetch_add(&st->sweep_tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t != (unsigned)nblocks - 1u) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    unsigned long long* rs = &st->residual[slot + i];
-    const unsigned long long bits = __hip_atomic_load(rs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // read and reset in one exchange (an idempotent read-modify-write would
+    // be lowered to a plain load, which may hit this XCD's L2)
+    const unsigned long long bits =
+        __hip_atomic_exchange(&st->residual[slot + i], kResidualInitBits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     check_convergence_scalar(st, __builtin_bit_cast(double, (long long)bits));
-    __hip_atomic_store(rs, kResidualInitBits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __hip_atomic_store(&st->sweep_tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  (void)__hip_atomic_exchange(&st->sweep_tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Workgroup-level commit of K residual slots: one wave max per slot into LDS,
