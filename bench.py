@@ -237,12 +237,16 @@ def run_rank(args) -> int:
     else:
         dims = tuple(int(v) for v in args.decomp.lower().split("x"))
 
+    # the per-stream graphs' mode: a canary deadlock (HeatSolver.initialize
+    # rebuilt that solver eagerly) turns them off for the later solvers too
+    sg_mode = [args.stream_graphs]
+
     def make(eps, iter_max, extra=(), decomp=None):
         return HeatSolver(N, iter_max=iter_max, eps=eps, dtype=args.dtype, backend="hip",
                           decomp=decomp or dims, kernel=args.kernel, graph=not args.no_graph,
                           overlap=not args.no_overlap, graph_chunk=args.graph_chunk,
                           device=dev, group=group, virtual_ranks=args.virtual_ranks, comm=args.comm,
-                          extra_args=["--stream-graphs", args.stream_graphs, "--graph-canary", str(args.graph_canary),
+                          extra_args=["--stream-graphs", sg_mode[0], "--graph-canary", str(args.graph_canary),
                                       "--temporal", str(args.temporal), "--kernel2", args.kernel2,
                                       "--watchdog", str(args.watchdog), "--reserve-cus", str(args.reserve_cus)]
                           + args.solver_flags.split() + list(extra))
@@ -262,6 +266,8 @@ def run_rank(args) -> int:
         for d in cands:
             t = make(0.0, 1 << 40, decomp=d)
             t.initialize()
+            if t.stream_graphs_retried:
+                sg_mode[0] = "off"
             t.step(esteps)
             t.prepare_steps(esteps)
             t.synchronize()
@@ -294,6 +300,8 @@ def run_rank(args) -> int:
 
     s = make(0.0, 1 << 40)
     s.initialize()
+    if s.stream_graphs_retried:
+        sg_mode[0] = "off"
     phase("initialize")
     s.step(max(1, args.warmup))
     phase("warmup enqueued")
@@ -343,6 +351,8 @@ def run_rank(args) -> int:
     esize = 8 if args.dtype == "fp64" else 4
     kernel = s.kernel
     sg_state, sg_note = s.native.stream_graphs_state, s.native.stream_graphs_note
+    if s.stream_graphs_retried or (args.stream_graphs != "off" and sg_mode[0] == "off"):
+        sg_state, sg_note = "fallback", "canary deadlock: the solver was rebuilt with --stream-graphs off"
     per_dev = s.native.ranks_per_device
     comm_name = s.native.comm_name
     comm_ranks = s.native.comm_transport_ranks

@@ -63,6 +63,12 @@ class Backend {
   virtual float elapsed_ms(Event a, Event b) = 0;
   virtual void sync(StreamId s) = 0;
   virtual void sync_all() = 0;
+  // sync_all bounded by a host-side deadline: false if some stream is still
+  // busy after `seconds` (its work keeps running)
+  virtual bool sync_all_for(double /*seconds*/) {
+    sync_all();
+    return true;
+  }
 
   // Graph recording: between begin_capture and end_capture nothing runs.
   //   * one graph (per_stream = false): every operation on any stream becomes

@@ -37,7 +37,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
+#include <thread>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -310,6 +312,19 @@ class HipBackend final : public Backend {
   void sync(StreamId s) override { HIP_CHECK(hipStreamSynchronize(streams_[s])); }
   void sync_all() override {
     for (auto& s : streams_) HIP_CHECK(hipStreamSynchronize(s));
+  }
+  bool sync_all_for(double seconds) override {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (auto& s : streams_) {
+      for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) HIP_CHECK(e);
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > seconds) return false;
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+      }
+    }
+    return true;
   }
 
   bool supports_graphs() const override { return true; }

@@ -675,9 +675,26 @@ void Solver::canary_stream_graphs() {
   prepare_steps(G);
   const int64_t launches = graph_launches_;
   comm_->barrier(*be_);
+  // The device-side waits give up after --graph-canary, but RCCL's own
+  // kernels wait for their peers without a limit: on a GPU whose hardware
+  // queues are oversubscribed (8 ranks of a rehearsal on one device) a peer's
+  // transfer kernel may never be scheduled behind a spinning wait, and the
+  // replay never ends (round 6, gpurun_out/r6f).  So the host bounds it too:
+  // past the limit the communicators are aborted (RCCL's kernels exit on the
+  // abort flag, the waits on their timeout) and initialize() throws; the
+  // vote below is bounded the same way for ranks whose replay ended while a
+  // peer's did not.  HeatSolver.initialize() then rebuilds the solver with
+  // the graphs off (a new communicator), every rank alike.
+  const double host_limit = std::max(10.0 + 4.0 * cfg_.graph_canary_s, 20.0 * eager);
+  auto deadlock = [&](const char* where) {
+    comm_->abort();
+    (void)be_->sync_all_for(2.0 * cfg_.graph_canary_s + 5.0);
+    HEAT3D_THROW("stream-graph canary deadlock: the per-stream hipGraph replay " << where << " within " << host_limit
+                 << " s (oversubscribed hardware queues?); communicators aborted; rerun with --stream-graphs off");
+  };
   t0 = now_s();
   run_chunk(G);
-  be_->sync_all();
+  if (!be_->sync_all_for(host_limit)) deadlock("did not finish");
   const double graph = now_s() - t0;
   sg_unchecked_ = false;
   be_->copy(hstate_, dstate_, offsetof(DeviceState, hist), CopyKind::D2H, kCompute);
@@ -687,8 +704,16 @@ void Solver::canary_stream_graphs() {
   const bool slow = graph > 2.0 * eager + 1e-3;
   // one decision for the job: the ranks' schedules must stay the same kind
   // (their collectives pair up either way, but a mixed job has no use)
-  const unsigned long long vote =
-      allreduce_sum_u64((timed_out ? 1ull << 40 : 0ull) + (slow ? 1ull << 20 : 0ull) + (replayed ? 0ull : 1ull));
+  unsigned long long vote = (timed_out ? 1ull << 40 : 0ull) + (slow ? 1ull << 20 : 0ull) + (replayed ? 0ull : 1ull);
+  if (!comm_->all_local() && comm_->size() > 1) {
+    void* d = be_->alloc(8);
+    be_->copy(d, &vote, 8, CopyKind::H2D, kReduce);
+    comm_->allreduce(d, 1, RedType::U64, RedOp::Sum, *be_, kReduce);
+    be_->copy(&vote, d, 8, CopyKind::D2H, kReduce);
+    const bool ok = be_->sync_all_for(host_limit);
+    if (ok) be_->release(d);
+    if (!ok) deadlock("vote did not complete (a peer's replay hung)");
+  }
   std::ostringstream os;
   os.setf(std::ios::fixed);
   os.precision(3);

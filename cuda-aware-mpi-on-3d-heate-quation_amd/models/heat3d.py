@@ -124,27 +124,48 @@ class HeatSolver:
             else:
                 comm = "local"
         if phantom is not None:
-            # performance proxy: rank phantom[0] of a phantom[1]-rank job, peers emulated
-            from ..parallel.distributed import NativeCommArgs
-
             comm = "phantom"
-            cargs = NativeCommArgs(int(phantom[0]), int(phantom[1]), "phantom")
-        elif comm in ("rccl", "socket", "staged"):
-            cargs = native_comm_args(comm, group=group)
-        else:
-            from ..parallel.distributed import NativeCommArgs
-
-            cargs = NativeCommArgs()
         dev = -1 if device is None else int(device)
         if use_gpu and device is None and info.world_size > 1:
             dev = info.local_rank % max(1, ext.device_count())
         self.comm_kind = comm
-        self._s = ext.Solver(args, device=dev, **cargs.kwargs())
+
+        def make(extra=()):
+            from ..parallel.distributed import NativeCommArgs
+
+            if phantom is not None:
+                # performance proxy: rank phantom[0] of a phantom[1]-rank job, peers emulated
+                cargs = NativeCommArgs(int(phantom[0]), int(phantom[1]), "phantom")
+            elif comm in ("rccl", "socket", "staged"):
+                cargs = native_comm_args(comm, group=group)  # collective: every rank calls it
+            else:
+                cargs = NativeCommArgs()
+            return ext.Solver(args + list(extra), device=dev, **cargs.kwargs())
+
+        self._make = make
+        self._s = make()
         self._initialized = False
+        self.stream_graphs_retried = False
 
     # -- lifecycle -------------------------------------------------------------
     def initialize(self) -> "HeatSolver":
-        self._s.initialize()
+        """(Re)initialise the fields.  If the start-up canary of the
+        overlapped schedule's per-stream hipGraphs deadlocks (the solver aborts
+        its communicators and raises; every rank alike), the native solver is
+        rebuilt once with the graphs off — a new communicator — and
+        initialised again: the run continues eagerly in this process."""
+        try:
+            self._s.initialize()
+        except RuntimeError as e:
+            if "stream-graph canary deadlock" not in str(e) or self.stream_graphs_retried:
+                raise
+            import sys
+
+            print(f"heat3d: {e}; rebuilding the solver with --stream-graphs off", file=sys.stderr, flush=True)
+            self.stream_graphs_retried = True
+            self._s = None
+            self._s = self._make(["--stream-graphs", "off"])
+            self._s.initialize()
         self._initialized = True
         return self
 
