@@ -177,6 +177,23 @@ std::string KernelSpec::str() const {
 }
 
 // ---------------------------------------------------------------------------
+static bool trace_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT3D_TRACE");
+    return e && *e && e[0] != '0';
+  }();
+  return on;
+}
+#define H3D_TRACE(msg)                                                   \
+  do {                                                                   \
+    if (trace_on()) {                                                    \
+      std::ostringstream _os;                                            \
+      _os << "[heat3d trace] " << msg << "\n";                           \
+      std::fputs(_os.str().c_str(), stderr);                             \
+      std::fflush(stderr);                                               \
+    }                                                                    \
+  } while (0)
+
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -687,14 +704,19 @@ void Solver::canary_stream_graphs() {
   // the graphs off (a new communicator), every rank alike.
   const double host_limit = std::max(10.0 + 4.0 * cfg_.graph_canary_s, 20.0 * eager);
   auto deadlock = [&](const char* where) {
+    H3D_TRACE("canary: " << where << " after " << host_limit << " s: aborting the communicators");
     comm_->abort();
-    (void)be_->sync_all_for(2.0 * cfg_.graph_canary_s + 5.0);
+    H3D_TRACE("canary: communicators aborted");
+    const bool drained = be_->sync_all_for(2.0 * cfg_.graph_canary_s + 5.0);
+    H3D_TRACE("canary: streams " << (drained ? "drained" : "still busy"));
     HEAT3D_THROW("stream-graph canary deadlock: the per-stream hipGraph replay " << where << " within " << host_limit
                  << " s (oversubscribed hardware queues?); communicators aborted; rerun with --stream-graphs off");
   };
+  H3D_TRACE("canary: eager cycle " << eager * 1e3 << " ms, graph captured; replaying (host limit " << host_limit << " s)");
   t0 = now_s();
   run_chunk(G);
   if (!be_->sync_all_for(host_limit)) deadlock("did not finish");
+  H3D_TRACE("canary: replay done in " << (now_s() - t0) * 1e3 << " ms");
   const double graph = now_s() - t0;
   sg_unchecked_ = false;
   be_->copy(hstate_, dstate_, offsetof(DeviceState, hist), CopyKind::D2H, kCompute);
@@ -1138,22 +1160,6 @@ void Solver::enqueue_halo_phase(int p, StreamId s, int dv, Pred in_phase) {
   }
 }
 
-static bool trace_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("HEAT3D_TRACE");
-    return e && *e && e[0] != '0';
-  }();
-  return on;
-}
-#define H3D_TRACE(msg)                                                   \
-  do {                                                                   \
-    if (trace_on()) {                                                    \
-      std::ostringstream _os;                                            \
-      _os << "[heat3d trace] " << msg << "\n";                           \
-      std::fputs(_os.str().c_str(), stderr);                             \
-      std::fflush(stderr);                                               \
-    }                                                                    \
-  } while (0)
 
 void Solver::enqueue_iteration(int p, int bi) {
   H3D_TRACE("iteration issued=" << issued_ << " parity=" << p << " buf=" << bi
