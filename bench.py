@@ -350,6 +350,7 @@ def run_rank(args) -> int:
     value = points * args.steps / dt / 1e9
     esize = 8 if args.dtype == "fp64" else 4
     kernel = s.kernel
+    runtime = heat3d_amd.runtime()  # after the backend set the device's host-wait mode
     sg_state, sg_note = s.native.stream_graphs_state, s.native.stream_graphs_note
     if s.stream_graphs_retried or (args.stream_graphs != "off" and sg_mode[0] == "off"):
         sg_state, sg_note = "fallback", "canary deadlock: the solver was rebuilt with --stream-graphs off"

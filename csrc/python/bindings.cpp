@@ -225,6 +225,7 @@ PYBIND11_MODULE(_heat3d, m) {
     d["hip_runtime_version"] = h.runtime_version;
     d["hip_driver_version"] = h.driver_version;
     d["hip_library"] = h.library;
+    d["sync_wait"] = h.sync_wait;
     d["rccl_version"] = rccl_version();
     d["rccl_library"] = rccl_library_path();
     return d;

@@ -145,6 +145,7 @@ int hip_device_count();  // 0 when no GPU / no driver
 struct HipRuntimeInfo {
   int runtime_version = 0, driver_version = 0;
   std::string library;
+  std::string sync_wait;  // the device's host-wait scheduling (spin / yield / blocking / auto)
 };
 HipRuntimeInfo hip_runtime_info();
 // block until every stream of `device` is idle (hipDeviceSynchronize)

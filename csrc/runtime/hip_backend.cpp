@@ -67,6 +67,14 @@ HipRuntimeInfo hip_runtime_info() {
   HipRuntimeInfo r;
   if (hipRuntimeGetVersion(&r.runtime_version) != hipSuccess) (void)hipGetLastError();
   if (hipDriverGetVersion(&r.driver_version) != hipSuccess) (void)hipGetLastError();
+  unsigned flags = 0;
+  if (hip_device_count() > 0 && hipGetDeviceFlags(&flags) == hipSuccess) {
+    const unsigned s = flags & hipDeviceScheduleMask;
+    r.sync_wait = s == hipDeviceScheduleSpin ? "spin" : s == hipDeviceScheduleYield ? "yield"
+                  : s == hipDeviceScheduleBlockingSync ? "blocking" : "auto";
+  } else {
+    (void)hipGetLastError();
+  }
   Dl_info di;
   if (dladdr(reinterpret_cast<void*>(&hipRuntimeGetVersion), &di) && di.dli_fname) {
     char buf[4096];
@@ -105,6 +113,18 @@ class HipBackend final : public Backend {
     HEAT3D_CHECK(n > 0, "no HIP device visible");
     HEAT3D_CHECK(device >= 0 && device < n, "device " << device << " out of range (" << n << " visible)");
     HIP_CHECK(hipSetDevice(dev_));
+    // How the host waits for the device (synchronize, event sync): spin by
+    // default.  With HIP's auto heuristic (fewer contexts than cores: yield)
+    // HIP 7.2 woke the bench's final synchronize late — the same graph timed
+    // 815.8 GLUPS against 844.0 under torch's HIP 7.0 on one box while the
+    // device-side sweep timings were equal (gpurun_out/r6f).
+    // HEAT3D_SYNC_WAIT=auto|yield|spin overrides.
+    {
+      const char* e = std::getenv("HEAT3D_SYNC_WAIT");
+      const std::string m = e && *e ? e : "spin";
+      const unsigned f = m == "auto" ? hipDeviceScheduleAuto : m == "yield" ? hipDeviceScheduleYield : hipDeviceScheduleSpin;
+      if (hipSetDeviceFlags(f) != hipSuccess) (void)hipGetLastError();  // already active: keep the process's
+    }
     int least = 0, greatest = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIP_CHECK(hipStreamCreateWithPriority(&streams_[kCompute], hipStreamNonBlocking, least));
