@@ -8,6 +8,8 @@ ranks of ``bench.py --gpus 2 --comm rccl``) the dispatches are classified as
   boundary  the other stencil dispatches (x-slab / shell pieces, comm stream)
   rccl      RCCL kernels (halo send/recv groups, all-reduce)
   check     the convergence check kernel
+  wait      graph_wait_kernel: a per-stream graph's device-side wait for another stream
+  signal    graph_signal_kernel: the signal it waits for
   other     pack / unpack / copies / anything else
 
 and the report gives, per process: count, median duration and the hardware
@@ -30,8 +32,12 @@ def classify(name, interior_grid, grid):
     n = name.lower()
     if "nccl" in n:
         return "rccl"
-    if "check_convergence" in n:
+    if "check_convergence" in n or "check_kernel" in n:
         return "check"
+    if "graph_wait" in n:
+        return "wait"
+    if "graph_signal" in n:
+        return "signal"
     if "stencil" in n:
         return "interior" if grid == interior_grid else "boundary"
     return "other"
@@ -71,7 +77,7 @@ def report(path):
     print(f"{len(rows)} dispatches; interior = stencil dispatches with grid {interior_grid}\n")
     print("| class | dispatches | median µs | total ms | queue ids | stream ids | time under an interior dispatch |")
     print("|---|---|---|---|---|---|---|")
-    for c in ("interior", "boundary", "rccl", "check", "other"):
+    for c in ("interior", "boundary", "rccl", "check", "wait", "signal", "other"):
         rs = by.get(c, [])
         if not rs:
             continue
@@ -86,6 +92,23 @@ def report(path):
             ov = f"{100.0 * o / max(1, tot):.1f} %"
         print(f"| {c} | {len(rs)} | {statistics.median(durs):.1f} | {tot / 1e6:.3f} | {', '.join(q)} | "
               f"{', '.join(s)} | {ov} |")
+    # stream -> hardware queue: a device-side wait must not share a queue with
+    # the stream that signals it (its signal would queue behind the spin)
+    sq = collections.defaultdict(set)
+    scls = collections.defaultdict(collections.Counter)
+    for r in rows:
+        sq[r.get("Stream_Id", "?")].add(r.get("Queue_Id", "?"))
+        scls[r.get("Stream_Id", "?")][r["_c"]] += 1
+    print("\n| stream id | queue ids | dispatches by class |\n|---|---|---|")
+    for s_id in sorted(sq):
+        print(f"| {s_id} | {', '.join(sorted(sq[s_id]))} | "
+              f"{', '.join(f'{c} {n}' for c, n in sorted(scls[s_id].items()))} |")
+    sync_streams = [s_id for s_id in sq if scls[s_id]["wait"] or scls[s_id]["signal"]]
+    shared = [(a, b) for i, a in enumerate(sync_streams) for b in sync_streams[i + 1:] if sq[a] & sq[b]]
+    if sync_streams:
+        print(f"\nstreams with graph waits / signals: {', '.join(sorted(sync_streams))}; "
+              + ("**share a hardware queue: " + "; ".join(f"{a} & {b}" for a, b in shared) + "**" if shared
+                 else "each on hardware queues of its own (no wait can queue behind its signaller)"))
     names = collections.Counter((r["_c"], r["Kernel_Name"][:110]) for r in rows)
     print("\n| class | kernel | dispatches |\n|---|---|---|")
     for (c, k), n in sorted(names.items()):
