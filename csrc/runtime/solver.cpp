@@ -1,6 +1,7 @@
 #include "solver.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstddef>
@@ -705,7 +706,27 @@ void Solver::canary_stream_graphs() {
   const double host_limit = std::max(10.0 + 4.0 * cfg_.graph_canary_s, 20.0 * eager);
   auto deadlock = [&](const char* where) {
     H3D_TRACE("canary: " << where << " after " << host_limit << " s: aborting the communicators");
-    comm_->abort();
+    // ncclCommAbort itself can hang on such a GPU (8 processes of a one-GPU
+    // rehearsal with the graphs forced on: it never returned, gpurun_out/r6h):
+    // run it on a helper thread and, if it does not return, end the process
+    // with a clear error instead of hanging the job
+    std::atomic<bool> aborted{false};
+    std::thread t([&] {
+      comm_->abort();
+      aborted = true;
+    });
+    const double ta = now_s();
+    while (!aborted && now_s() - ta < 10.0) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    if (!aborted) {
+      std::fprintf(stderr,
+                   "heat3d: stream-graph canary deadlock: the per-stream hipGraph replay %s within %.1f s and "
+                   "ncclCommAbort did not return in 10 s (oversubscribed GPU?); exiting — rerun with "
+                   "--stream-graphs off\n",
+                   where, host_limit);
+      std::fflush(stderr);
+      std::_Exit(86);
+    }
+    t.join();
     H3D_TRACE("canary: communicators aborted");
     const bool drained = be_->sync_all_for(2.0 * cfg_.graph_canary_s + 5.0);
     H3D_TRACE("canary: streams " << (drained ? "drained" : "still busy"));
