@@ -311,6 +311,12 @@ def run_rank(args) -> int:
     s.prepare_steps(args.steps)
     phase("graphs prepared")
     s.synchronize()
+    # the process's first device-wide synchronize costs ~1.4 s under HIP 7.2
+    # (a one-time lazy initialisation; torch's HIP 7.0 took ~18 ms): pay it
+    # here, not in the barrier right before the timed window, where the GPU
+    # then idled and clocked down (the first timed sweeps ran 10 % slow;
+    # gpurun_out/r6h, r6i)
+    ext.device_synchronize(dev)
     phase("warmup synchronized")
     # race detection before timing: every face sent by the warm-up exchange
     # must match, bit for bit, the ghost layer the neighbour received
