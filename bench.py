@@ -311,11 +311,6 @@ def run_rank(args) -> int:
     s.prepare_steps(args.steps)
     phase("graphs prepared")
     s.synchronize()
-    # the process's first device-wide synchronize costs ~1.4 s under HIP 7.2
-    # (a one-time lazy initialisation; torch's HIP 7.0 took ~18 ms): pay it
-    # here, not in the barrier right before the timed window, where the GPU
-    # then idled and clocked down (the first timed sweeps ran 10 % slow;
-    # gpurun_out/r6h, r6i)
     ext.device_synchronize(dev)
     phase("warmup synchronized")
     # race detection before timing: every face sent by the warm-up exchange
@@ -338,6 +333,13 @@ def run_rank(args) -> int:
                if args.preheat_ms > 0 else 0)
     phase("preheat enqueued")
     barrier(group)
+    # HIP 7.2's hipDeviceSynchronize over in-flight work (the preheat) woke
+    # ~1.4 s after the GPU had finished (18 ms of sweeps; torch's HIP 7.0:
+    # 18 ms in all), and the GPU idled and clocked down before the timed
+    # window: its first sweeps ran ~10 % slow (gpurun_out/r6h trace, r6i /
+    # r6j phases).  Stream synchronisation wakes on time; the device-wide
+    # synchronize then finds nothing in flight.
+    s.synchronize()
     ext.device_synchronize(dev)
     phase("barrier")
     t0 = time.perf_counter()
