@@ -20,6 +20,7 @@ from __future__ import annotations
 import json
 import os
 import socket
+import sys
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -181,13 +182,19 @@ def native_comm_args(kind: str, group=None) -> NativeCommArgs:
     raise ValueError(f"unknown native comm kind {kind!r}")
 
 
+def _torch_dist():
+    """torch.distributed if this process initialised it, else None — without
+    importing torch (a torch-free rank must not load torch's HIP runtime)."""
+    dist = sys.modules.get("torch.distributed")
+    return dist if dist is not None and dist.is_initialized() else None
+
+
 def barrier(group=None):
     if isinstance(group, HostGroup):
         group.barrier()
         return
-    import torch.distributed as dist
-
-    if dist.is_initialized():
+    dist = _torch_dist()
+    if dist is not None:
         dist.barrier(group=group)
 
 
@@ -196,9 +203,8 @@ def all_gather_objects(obj, group=None) -> list:
     pickle); [obj] alone."""
     if isinstance(group, HostGroup):
         return group.allgather(obj)
-    import torch.distributed as dist
-
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    dist = _torch_dist()
+    if dist is None or dist.get_world_size() == 1:
         return [obj]
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, obj, group=group)
@@ -209,11 +215,11 @@ def max_over_ranks(value: float, group=None) -> float:
     """Host-side max of a scalar over ranks (HostGroup or gloo bootstrap group)."""
     if isinstance(group, HostGroup):
         return group.max(value)
-    import torch
-    import torch.distributed as dist
-
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    dist = _torch_dist()
+    if dist is None or dist.get_world_size() == 1:
         return value
+    import torch
+
     dev = "cpu"
     if group is None and dist.get_backend() == "nccl":
         dev = torch.device("cuda", torch.cuda.current_device())
