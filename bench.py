@@ -332,13 +332,13 @@ def run_rank(args) -> int:
     preheat = (s.native.preheat(max(1, min(64, int(args.preheat_ms / max(est_ms, 1e-3)) + 1)))
                if args.preheat_ms > 0 else 0)
     phase("preheat enqueued")
+    # nothing between the preheat and the timed window may take host time: a
+    # barrier that imported torch (~1.4 s, the single-process path of the
+    # host collectives before round 6's fix) idled the GPU, which clocked
+    # down, and the first timed sweeps ran ~10 % slow (gpurun_out/r6h trace,
+    # r6i-r6k phases; tools/probes/sync_wake_probe.hip: the waits themselves
+    # wake on time)
     barrier(group)
-    # HIP 7.2's hipDeviceSynchronize over in-flight work (the preheat) woke
-    # ~1.4 s after the GPU had finished (18 ms of sweeps; torch's HIP 7.0:
-    # 18 ms in all), and the GPU idled and clocked down before the timed
-    # window: its first sweeps ran ~10 % slow (gpurun_out/r6h trace, r6i /
-    # r6j phases).  Stream synchronisation wakes on time; the device-wide
-    # synchronize then finds nothing in flight.
     s.synchronize()
     ext.device_synchronize(dev)
     phase("barrier")

@@ -113,12 +113,10 @@ class HipBackend final : public Backend {
     HEAT3D_CHECK(n > 0, "no HIP device visible");
     HEAT3D_CHECK(device >= 0 && device < n, "device " << device << " out of range (" << n << " visible)");
     HIP_CHECK(hipSetDevice(dev_));
-    // How the host waits for the device (synchronize, event sync): spin by
-    // default.  With HIP's auto heuristic (fewer contexts than cores: yield)
-    // HIP 7.2 woke the bench's final synchronize late — the same graph timed
-    // 815.8 GLUPS against 844.0 under torch's HIP 7.0 on one box while the
-    // device-side sweep timings were equal (gpurun_out/r6f).
-    // HEAT3D_SYNC_WAIT=auto|yield|spin overrides.
+    // How the host waits for the device (synchronize, event sync): spin, the
+    // lowest wake-up latency, whatever HIP's auto heuristic would pick for
+    // the host's core count (on the 1-GPU boxes it picks spin too:
+    // tools/probes/sync_wake_probe.hip).  HEAT3D_SYNC_WAIT=auto|yield|spin.
     {
       const char* e = std::getenv("HEAT3D_SYNC_WAIT");
       const std::string m = e && *e ? e : "spin";
