@@ -44,3 +44,17 @@ def test_runtime_policy_refuses_torch_first(tmp_path):
             "sys.exit(1)") % os.path.dirname(HERE)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "refused" in r.stdout, (r.stdout, r.stderr)
+
+
+def test_single_process_collectives_do_not_import_torch():
+    """bench.py at N = 1 calls the host collectives with no group: they must
+    not import torch (round 6: a barrier that did cost ~1.4 s right before the
+    timed window and loaded torch's second HIP runtime into the process)."""
+    code = ("import sys, os; sys.path.insert(0, %r); os.environ['HEAT3D_RUNTIME'] = 'rocm'\n"
+            "import heat3d_amd\n"
+            "from heat3d_amd.parallel.distributed import barrier, all_gather_objects, max_over_ranks\n"
+            "barrier(None); assert all_gather_objects({'a': 1}, None) == [{'a': 1}]; assert max_over_ranks(2.0) == 2.0\n"
+            "assert 'torch' not in sys.modules, sorted(m for m in sys.modules if m.startswith('torch'))[:5]\n"
+            "print('ok')") % os.path.dirname(HERE)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout, r.stderr)
