@@ -132,7 +132,8 @@ std::string Config::usage() {
      << "  --no-rccl-graph           never record RCCL calls into hipGraphs (eager multi-rank steps)\n"
      << "  --rccl-shared             one RCCL communicator for halos and all-reduces\n"
      << "  --rccl-p2p-channels N     RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS unless set in the\n"
-     << "                            environment): N > 0 that many; default RCCL's own\n"
+     << "                            environment): N > 0 that many; default RCCL's own (8 on the 2-rank\n"
+     << "                            one-GPU rehearsal under RCCL 2.27 drove host memory past 270 GB)\n"
      << "  --mem-reserve-gb G        memory preflight reserve (default 2)\n"
      << "  --no-mem-preflight        skip the memory preflight\n"
      << "  --host-mem-limit-gb G     host RAM budget of the gather-to-root Tecplot (default RAM/2)\n"

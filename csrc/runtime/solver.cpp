@@ -1005,8 +1005,15 @@ void Solver::calibrate_remainders() {
   // votes for the partial sweep, one slot per remainder; the ranks agree on
   // the max: long only where no rank found the partial sweep cheaper (the
   // halo depth of every exchange must match between neighbours)
+  // With halos the timed interiors understate a long sweep: it also moves
+  // (K+1)-deep halos and thicker boundary slabs.  On the 8-GPU slab share
+  // (phantom rank, driver window) long sweeps for r = 2 timed 5 % cheaper than
+  // the partial one (0.434 vs 0.456 ms) and ran the window 7 % slower (0.2400
+  // against 0.2234 ms/step, gpurun_out/r6o): a long remainder must win by
+  // 15 % there.
+  const double margin = has_halo_ ? 1.15 : 1.0;
   std::vector<unsigned long long> partial(K_, 0);
-  for (int r = 1; r < K_; ++r) partial[r] = r * (tl - tk) < cost[r] ? 0 : 1;
+  for (int r = 1; r < K_; ++r) partial[r] = r * (tl - tk) * margin < cost[r] ? 0 : 1;
   if (!comm_->all_local() && comm_->size() > 1) {
     void* d = be_->alloc(sizeof(unsigned long long) * K_);
     be_->copy(d, partial.data(), sizeof(unsigned long long) * K_, CopyKind::H2D, kReduce);
