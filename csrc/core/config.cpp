@@ -122,8 +122,9 @@ std::string Config::usage() {
      << "  --autotune auto|on|off    time the sweep schedule candidates (z stride, x segments) at start-up;\n"
      << "                            auto: single-subdomain runs (--no-autotune = off)\n"
      << "  --stream-graphs auto|on|off  the overlapped multi-stream schedule as one linear hipGraph per\n"
-     << "                            stream with device-side cross-stream waits (auto: on unless more than\n"
-     << "                            4 ranks share a GPU; --no-stream-graphs = off), verified at start-up\n"
+     << "                            stream with device-side cross-stream waits, verified at start-up\n"
+     << "                            (auto = off: eager measured faster on the 8-GPU share; on = graphs;\n"
+     << "                            --no-stream-graphs = off)\n"
      << "  --graph-canary S          device-wait timeout of the start-up canary replay of those graphs; a\n"
      << "                            rank whose replay times out or runs > 2x eager turns them off for the\n"
      << "                            job (default 2; 0 = no canary)\n"

@@ -87,8 +87,8 @@ struct Config {
   // (single-subdomain runs, whose sweeps run alone as they are timed), 0 off, 1 on
   int autotune = -1;
   // overlapped multi-stream schedules as hipGraphs too (one linear graph per
-  // stream, device-side cross-stream waits): -1 auto (on unless more than 4
-  // ranks share a GPU: oversubscribed hardware queues), 1 on, 0 eager.  Where
+  // stream, device-side cross-stream waits): -1 auto (eager: measured faster
+  // on the 8-GPU share, Solver::stream_graphs_enabled), 1 on, 0 eager.  Where
   // on, a canary replay at initialisation with a short device-wait timeout
   // (graph_canary_s) decides; a timed-out or pathologically slow replay on any
   // rank turns them off for the job (Solver::canary_stream_graphs).

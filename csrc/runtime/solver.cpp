@@ -1645,12 +1645,20 @@ bool Solver::graphs_allowed() const {
          !force_eager_ && (!multi_stream() || stream_graphs_enabled());
 }
 
-// --stream-graphs auto: on unless more than 4 processes share the GPU (the
-// 8-rank one-GPU rehearsal oversubscribed its hardware queues and hung with
-// them, round 5); the canary has the last word either way
+// --stream-graphs auto replays the overlapped multi-stream schedule eagerly:
+// on the 8-GPU slab share (phantom rank, driver window) eager ran 0.2233 /
+// 0.2240 ms/step against 0.2314 / 0.2308 with the per-stream graphs (each
+// launch joins and re-forks the streams, which drains the halo pipeline once:
+// ~0.12 ms per launch; gpurun_out/r6p), and over 300 steps 0.2086 against
+// 0.2115 (round 5) — the graphs' cheaper cross-stream waits (13 / 10 us per
+// sweep against 31 / 41, profiles/r06/chain_gaps_8gpu_share.md) do not pay
+// for it — and their device-side waits are a liveness hazard where queues are
+// shared.  "on" records them (canary-verified), unless more than 4 processes
+// share the GPU (the 8-rank one-GPU rehearsal oversubscribes its hardware
+// queues: round 5's hang, round 6's canary deadlock).
 bool Solver::stream_graphs_enabled() const {
-  if (sg_fallback_ || cfg_.stream_graphs == 0) return false;
-  return cfg_.stream_graphs == 1 || ranks_per_device_ <= 4;
+  if (sg_fallback_ || cfg_.stream_graphs != 1) return false;
+  return true;
 }
 
 Solver::GraphEntry* Solver::find_graph(int G) {

@@ -73,7 +73,7 @@ def test_stream_graph_wait_timeout_flags_fault(h3d, gpu):
     s = h3d.HeatSolver((64, 64, 64), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(1, 8),
                        graph_chunk=6,
                        extra_args=["--phantom-gbps", "4e-5", "--phantom-allreduce-us", "1", "--watchdog", "0.5",
-                                   "--long-sweeps", "off", "--lag", "off", "--graph-canary", "0"])
+                                   "--long-sweeps", "off", "--lag", "off", "--graph-canary", "0", "--stream-graphs", "on"])
     s.initialize()
     assert s.native.stream_graphs_state == "unverified"
     g0 = s.native.graph_launches
@@ -98,7 +98,7 @@ def test_stream_graph_canary_falls_back_to_eager(h3d, gpu):
     args = ["--phantom-gbps", "2e-4", "--phantom-allreduce-us", "1", "--long-sweeps", "off", "--lag", "off"]
     t0 = time.perf_counter()
     s = h3d.HeatSolver((64, 64, 64), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(1, 8),
-                       graph_chunk=6, extra_args=args + ["--graph-canary", "0.2"])
+                       graph_chunk=6, extra_args=args + ["--graph-canary", "0.2", "--stream-graphs", "on"])
     s.initialize()
     el = time.perf_counter() - t0
     assert s.native.stream_graphs_state == "fallback", s.native.stream_graphs_note
@@ -131,7 +131,7 @@ def test_stream_graph_canary_passes(h3d, gpu):
 
     args = ["--phantom-gbps", "50", "--long-sweeps", "off"]
     s = h3d.HeatSolver((96, 96, 96), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(2, 8),
-                       extra_args=args)
+                       extra_args=args + ["--stream-graphs", "on"])
     s.initialize()
     assert s.native.stream_graphs_state == "on", s.native.stream_graphs_note
     assert "graphs" in s.native.stream_graphs_note and "eager" in s.native.stream_graphs_note
@@ -147,3 +147,23 @@ def test_stream_graph_canary_passes(h3d, gpu):
     e.step(36)
     e.synchronize()
     assert np.array_equal(s.local_field(0, True), e.local_field(0, True))
+
+
+def test_stream_graphs_auto_is_eager(h3d, gpu):
+    """--stream-graphs auto replays the overlapped multi-rank schedule eagerly
+    (measured faster on the 8-GPU share: Solver::stream_graphs_enabled); the
+    single-stream schedule keeps its graph."""
+    s = h3d.HeatSolver((96, 96, 96), 1 << 40, 0.0, backend="hip", device=0, decomp=(8, 1, 1), phantom=(2, 8),
+                       extra_args=["--phantom-gbps", "50"])
+    s.initialize()
+    assert s.native.stream_graphs_state == "off", s.native.stream_graphs_note
+    g0 = s.native.graph_launches
+    s.step(36)
+    s.synchronize()
+    assert s.native.graph_launches == g0
+    one = h3d.HeatSolver((96, 96, 96), 1 << 40, 0.0, backend="hip", device=0)
+    one.initialize()
+    assert one.native.stream_graphs_state == "n/a"
+    one.step(36)
+    one.synchronize()
+    assert one.native.graph_launches > 0

@@ -132,7 +132,7 @@ def test_rccl_graph_bitwise(h3d, gpu, tmp_path, world, decomp, schedule):
     the eager single-process solve bit for bit.  Reference per-iteration
     comm: heat3D.cu:619-641 (halo), 1062-1063 (reduction)."""
     n, eps = 33, 1e-4
-    extra = schedule + ["--rccl-graph", "--watchdog", "60"]
+    extra = schedule + ["--rccl-graph", "--watchdog", "60", "--stream-graphs", "on"]
     mp.start_processes(native_rccl_gpu_worker,
                        args=(world, free_port(), str(tmp_path), n, eps, decomp, "fp64", extra),
                        nprocs=world, join=True, start_method="spawn")
@@ -151,8 +151,8 @@ def test_rccl_8rank_blocks_bitwise(h3d, gpu, tmp_path, decomp, dtype):
     and sent through ncclSend / ncclRecv with real peers, axis-ordered 3-axis
     deep halos (edges and corners ride the later phases), the overlapped
     boundary onion and the lagged all-reduce — 8 processes on the one GPU,
-    eager replay (more than 4 ranks share the device: --stream-graphs auto
-    turns the per-stream graphs off).  Bitwise equal to the one-rank solve of
+    eager replay (--stream-graphs auto: the overlapped schedule's per-stream
+    graphs are opt-in, and never with more than 4 ranks on a device).  Bitwise equal to the one-rank solve of
     the same dtype, same stopping iteration.  eps 1e-2 (188 iterations): 8
     ranks on one GPU over RCCL's loopback network transport take ~80 ms per
     step (profiles/r06/rccl8_2x2x2_rehearsal.json).  Reference: heat3D.cu:243-263

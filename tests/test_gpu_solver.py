@@ -120,7 +120,7 @@ def test_virtual_ranks_bitwise(h3d, gpu, vr, decomp):
 def test_schedules_bitwise(h3d, gpu, graph, overlap):
     base, rb = _solve(h3d, 45, 1e-4, virtual_ranks=4, graph=False, overlap=False, check_every=1)
     s, r = _solve(h3d, 45, 1e-4, virtual_ranks=4, graph=graph, overlap=overlap, check_every=7,
-                  graph_chunk=6)
+                  graph_chunk=6, extra_args=["--stream-graphs", "on"])
     assert r["conv_iter"] == rb["conv_iter"]
     assert np.array_equal(s.gather(), base.gather())
 

@@ -467,7 +467,7 @@ def test_preheat_state_neutral_gpu(h3d, gpu, vr, dims, dtype):
     iteration count), graphs on, single domain / slabs (3 buffers) / 2x2x2."""
     n = (45, 61, 150)
     mk = lambda: h3d.HeatSolver(n, 10 ** 6, 0.0, dtype=dtype, backend="hip", virtual_ranks=vr, decomp=dims,
-                                graph_chunk=12)
+                                graph_chunk=12, extra_args=["--stream-graphs", "on"])
     for a_steps, b_steps in ((5, 20), (6, 12)):
         a, b = mk(), mk()
         a.initialize(), b.initialize()

@@ -41,7 +41,9 @@ def main() -> int:
     N = (args.n,) * 3
 
     def solve(graph: bool):
-        kw = dict(dtype=args.dtype, backend="hip", decomp=dims, graph=graph, graph_chunk=36, device=0)
+        # the overlapped schedules' per-stream graphs are opt-in (--stream-graphs on)
+        kw = dict(dtype=args.dtype, backend="hip", decomp=dims, graph=graph, graph_chunk=36, device=0,
+                  extra_args=["--stream-graphs", "on"])
         if args.phantom:
             r, p = (int(v) for v in args.phantom.split("/"))
             s = HeatSolver(N, iter_max=1 << 30, eps=0.0, phantom=(r, p), **kw)
