@@ -14,6 +14,12 @@
 //    for the last boundary slabs, the halo for the interior's buffer):
 //    A = [ticket a0, record e1, wait e2, ticket a1];
 //    B = [wait e1, spin, ticket b0, record e2].  Expected a0 < b0 < a1.
+// Observed on HIP 7.2.26015 (profiles/r06/graph_event_probe.log): case 1
+// ordered 5 of 5, case 2 unordered 5 of 5 (the wait node binds the event's
+// state when its graph is launched), case 3 aborts inside the runtime
+// (std::bad_alloc while capturing the second graph; an earlier build without
+// the pre-recorded events died with SIGSEGV there).  So event nodes cannot
+// replace the per-stream graphs' device-side waits.
 // Every kernel ends on its own (bounded spins); nothing waits on the device
 // for another kernel, so a dependency that does not hold shows as a wrong
 // order, never as a hang.  Host-side waits give up after 5 s.
