@@ -162,9 +162,12 @@ SLAB_MIN_LINK_GBPS = {8: 55.0}
 
 
 def choose_dims(N: Sequence[int], nprocs: int, link_gbps: Optional[float]) -> Tuple[int, int, int]:
-    """--decomp auto of the bench: slabs (best_dims_for) unless the job's
-    slowest measured link (Solver.link_probe, GB/s one way) is below the
-    proxy's crossover for this rank count, then the 2D block with the x
+    """Round 5's --decomp auto heuristic (kept as a documented rule, no
+    longer used by bench.py, which times every candidate grid since round 6:
+    decomp_candidates / pick_measured): slabs (best_dims_for) unless the
+    job's slowest measured link (Solver.link_probe, GB/s one way) is below
+    the phantom-rank proxy's crossover for this rank count — a proxy-derived
+    constant, not a measurement of real links — then the 2D block with the x
     extent halved and 2 ranks along y."""
     slab = best_dims_for(N, nprocs)
     cut = SLAB_MIN_LINK_GBPS.get(nprocs)
