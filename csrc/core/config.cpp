@@ -130,6 +130,9 @@ std::string Config::usage() {
      << "                            job (default 2; 0 = no canary)\n"
      << "  --no-fused-check          single-subdomain sweeps: a check kernel after each sweep instead of\n"
      << "                            the check in the sweep's last workgroup\n"
+     << "  --no-monotone-check       fused checks: every step's residual, not only each sweep's last one\n"
+     << "                            (the residual max-norm of FTCS never grows, so the last one decides;\n"
+     << "                            the converging sweep is replayed with all residuals for the iteration)\n"
      << "  --no-rccl-graph           never record RCCL calls into hipGraphs (eager multi-rank steps)\n"
      << "  --rccl-shared             one RCCL communicator for halos and all-reduces\n"
      << "  --rccl-p2p-channels N     RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS unless set in the\n"
@@ -284,6 +287,7 @@ Config Config::parse(int argc, const char* const* argv) {
     }
     else if (key == "--graph-canary") c.graph_canary_s = to_f64(get("--graph-canary"), "--graph-canary");
     else if (key == "--no-fused-check") c.fuse_check = false;
+    else if (key == "--no-monotone-check") c.monotone_check = false;
     else if (key == "--rccl-graph") c.rccl_graph = true;
     else if (key == "--no-rccl-graph") c.rccl_graph = false;
     else if (key == "--rccl-shared") c.rccl_shared = true;

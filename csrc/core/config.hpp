@@ -97,6 +97,9 @@ struct Config {
   // single-subdomain K-step sweeps run their convergence check in the sweep's
   // last workgroup (StencilParams::fuse_check) instead of a kernel after it
   bool fuse_check = true;
+  // ... and from each sweep's last residual only (the FTCS residual max-norm
+  // is non-increasing; Solver::residual_last_ok, resolve_coarse)
+  bool monotone_check = true;
   bool rccl_graph = true;         // RCCL calls may be recorded into hipGraphs (tests/test_gpu_rccl.py)
   bool rccl_shared = false;       // one RCCL communicator for halos and all-reduces (else ncclCommSplit)
   int rccl_p2p_channels = 0;      // RCCL P2P channel pool (NCCL_MAX_P2P_NCHANNELS): N > 0 that many, else RCCL's default

@@ -137,7 +137,13 @@ __device__ __forceinline__ void residual_commit(unsigned long long* slot, double
 // ticket (s_waitcnt), the state fields the last workgroup writes are read by
 // later kernels and the host, after this kernel's end-of-kernel release.
 // Every thread of the workgroup must reach it (barrier).
-template <int K>
+// RL (kResidualLastOnly): the sweep computed only its last step's residual.
+// The residual max-norm of FTCS is non-increasing (Solver::residual_last_ok),
+// so a last residual at or above the threshold means none of the sweep's
+// steps converged: steps 0..K-2 only advance the iteration; a last residual
+// below it sets done with conv_iter at the sweep's last iteration and
+// `coarse` = K, and Solver::resolve_coarse finds the first converged one.
+template <int K, bool RL = false>
 __device__ __forceinline__ void fused_check_tail(DeviceState* st, int slot, int nblocks) {
   __syncthreads();
   if (threadIdx.x != 0) return;
@@ -150,7 +156,13 @@ __device__ __forceinline__ void fused_check_tail(DeviceState* st, int slot, int 
     // be lowered to a plain load, which may hit this XCD's L2)
     const unsigned long long bits =
         __hip_atomic_exchange(&st->residual[slot + i], kResidualInitBits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (RL && i < K - 1) {
+      st->iter = st->iter + 1;
+      continue;
+    }
+    const int was = st->done;
     check_convergence_scalar(st, __builtin_bit_cast(double, (long long)bits));
+    if (RL && !was && st->done) st->coarse = K;
   }
   (void)__hip_atomic_exchange(&st->sweep_tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -63,6 +63,9 @@ struct Layout {
 // non-negative double so that an unsigned 64-bit atomic max (and an RCCL
 // uint64 max all-reduce) is an exact max of the doubles.
 constexpr int kResidualSlots = 8;
+// K-step sweep kernels: bit of the store-policy template argument (spec
+// field 7) that computes only the last step's residual (fused_check_tail)
+constexpr int kResidualLastOnly = 64;
 
 struct DeviceState {
   // max |T^{n+1}-T^n| accumulators: single steps use slot t & 1, a K-step
@@ -84,7 +87,10 @@ struct DeviceState {
   // workgroups that finished the current sweep; the last one runs the check
   // and resets it to 0
   uint32_t sweep_tickets;
-  uint32_t pad0;
+  // a sweep that computed only its last step's residual (kResidualLastOnly)
+  // set done: the first converged (or faulted) iteration is one of its last
+  // `coarse` iterations, conv_iter <= that; Solver::resolve_coarse finds it
+  uint32_t coarse;
   int64_t hist_cap;                // residual history ring capacity
   double hist[1024];               // residual history ring (index = iter % cap)
 };

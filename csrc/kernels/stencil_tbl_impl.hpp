@@ -125,10 +125,13 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
   // x-loop unroll making every ring index and the LDS parity static
   constexpr int U = lcm_l(lcm_l(Q, 3), 2);
   static_assert(YS > 0 && R <= 16, "tile too small for depth K");
+  // NTS bit kResidualLastOnly: only the last step's residual (monotone check)
+  constexpr bool RL = (NTS & kResidualLastOnly) != 0;
+  constexpr int ST = NTS & ~kResidualLastOnly;  // the stores' cache-policy bits
   __shared__ __attribute__((aligned(16))) Real s_row[2][K][WY][2][64];
   static_assert(sizeof(s_row) >= WY * K * sizeof(unsigned long long), "residual scratch");
   if (flag_set(done)) {
-    if (g.fst) fused_check_tail<K>(g.fst, g.fslot, g.fblocks);
+    if (g.fst) fused_check_tail<K, RL>(g.fst, g.fslot, g.fblocks);
     return;
   }
 
@@ -319,15 +322,17 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
           if constexpr (FAST) N[r] = nv;
           else N[r] = (upd && zin) ? nv : C[r];
         }
-        if constexpr (FAST) {
-          m[s] = fmax(m[s], d);
-        } else {
-          if (cnt) m[s] = fmax(m[s], d);
+        if (!RL || s == K - 1) {
+          if constexpr (FAST) {
+            m[s] = fmax(m[s], d);
+          } else {
+            if (cnt) m[s] = fmax(m[s], d);
+          }
         }
         if (s == K - 1 && st) {
           // T^{n+K} on the stored region (inside the box, hence the update range)
           nan_seen |= zst && (nv != nv);
-          if (zst) buf_store<Real, NTS>(nv, plane_rsrc(outw + (int64_t)p * sx), lane_b, r * sy_b);
+          if (zst) buf_store<Real, ST>(nv, plane_rsrc(outw + (int64_t)p * sx), lane_b, r * sy_b);
         }
       }
       if constexpr (Q == 3) {
@@ -363,7 +368,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbl(const Real* __restrict__ 
     residual_commit_block<WY, K>(res, mm, nan_seen,
                                  *reinterpret_cast<unsigned long long(*)[WY][K]>(&s_row[0][0][0][0][0]));
   }
-  if (g.fst) fused_check_tail<K>(g.fst, g.fslot, g.fblocks);
+  if (g.fst) fused_check_tail<K, RL>(g.fst, g.fslot, g.fblocks);
 }
 
 template <typename Real, int R, int WY, int K, int Q, int NTS = 0, bool SW = false>

@@ -147,10 +147,13 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const T* __restrict__ in,
   constexpr int YS = TY - 2 * K;       // tile stride along y (stored rows)
   constexpr int U = lcm_p(lcm_p(Q, 3), 2);
   static_assert(YS > 0 && R <= 16, "tile too small for depth K");
+  // AUX bit kResidualLastOnly: only the last step's residual (monotone check)
+  constexpr bool RL = (AUX & kResidualLastOnly) != 0;
+  constexpr int ST = AUX & ~kResidualLastOnly;  // the stores' cache-policy bits
   __shared__ __attribute__((aligned(16))) f2 s_row[2][K][WY][2][64];
   static_assert(sizeof(s_row) >= WY * K * sizeof(unsigned long long), "residual scratch");
   if (flag_set(done)) {
-    if (g.fst) fused_check_tail<K>(g.fst, g.fslot, g.fblocks);
+    if (g.fst) fused_check_tail<K, RL>(g.fst, g.fslot, g.fblocks);
     return;
   }
 
@@ -309,19 +312,21 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const T* __restrict__ in,
           if constexpr (FAST) N[r] = nv;
           else N[r] = f2{(upd && zin0) ? nv.x : c.x, (upd && zin1) ? nv.y : c.y};
         }
-        if constexpr (FAST) {
-          m[s] = __builtin_elementwise_max(m[s], d);
-        } else {
-          if (cnt) m[s] = __builtin_elementwise_max(m[s], d);
+        if (!RL || s == K - 1) {
+          if constexpr (FAST) {
+            m[s] = __builtin_elementwise_max(m[s], d);
+          } else {
+            if (cnt) m[s] = __builtin_elementwise_max(m[s], d);
+          }
         }
         if (s == K - 1 && st) {
           nan_seen |= (zst0 && nv.x != nv.x) || (zst1 && nv.y != nv.y);
           const __amdgpu_buffer_rsrc_t ro = prs(outw + (int64_t)p * sx);
           if (zst2) {
-            st2<AUX, T>(nv, ro, lane_b, r * sy_b);
+            st2<ST, T>(nv, ro, lane_b, r * sy_b);
           } else {
-            if (zst0) st1<AUX, T>(nv.x, ro, lane_b, r * sy_b);
-            if (zst1) st1<AUX, T>(nv.y, ro, lane_b + (unsigned)sizeof(T), r * sy_b);
+            if (zst0) st1<ST, T>(nv.x, ro, lane_b, r * sy_b);
+            if (zst1) st1<ST, T>(nv.y, ro, lane_b + (unsigned)sizeof(T), r * sy_b);
           }
         }
       }
@@ -355,7 +360,7 @@ __global__ __launch_bounds__(64 * WY) void stencil_tbp(const T* __restrict__ in,
     residual_commit_block<WY, K>(res, mm, nan_seen,
                                  *reinterpret_cast<unsigned long long(*)[WY][K]>(&s_row[0][0][0][0][0]));
   }
-  if (g.fst) fused_check_tail<K>(g.fst, g.fslot, g.fblocks);
+  if (g.fst) fused_check_tail<K, RL>(g.fst, g.fslot, g.fblocks);
 }
 
 // Tile stride along z: 128 - 2K - 2 stored columns (tiles start on even
@@ -533,6 +538,7 @@ static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) 
   if constexpr (sizeof(T) == 4) {
     // output-store cache policy (spec field 7), default shape only
     H3D_TBP(3, 16, 3, 3, 2) H3D_TBP(3, 16, 3, 3, 3) H3D_TBP(3, 16, 3, 3, 17) H3D_TBP(3, 16, 3, 3, 19)
+    H3D_TBP(3, 16, 3, 3, 2 | kResidualLastOnly)
     H3D_TBP(3, 16, 3, 3, 0) H3D_TBP(3, 16, 3, 4, 0) H3D_TBP(2, 16, 3, 3, 0) H3D_TBP(2, 16, 4, 3, 0)
     H3D_TBP(2, 16, 4, 4, 0) H3D_TBP(3, 16, 4, 3, 0) H3D_TBP(2, 16, 2, 3, 0) H3D_TBP(3, 16, 2, 3, 0)
   } else {
@@ -542,6 +548,7 @@ static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) 
     // LDS), K = 2 in 6 rows and K = 4 in 3 rows of 8 waves; nt stores (2) or
     // default (0)
     H3D_TBP(4, 8, 3, 3, 2) H3D_TBP(4, 8, 3, 3, 0) H3D_TBP(6, 8, 2, 3, 2)
+    H3D_TBP(4, 8, 3, 3, 2 | kResidualLastOnly)
     H3D_TBP(3, 8, 4, 3, 2)
   }
 #undef H3D_TBP

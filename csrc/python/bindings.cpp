@@ -749,6 +749,7 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("stream_graphs_state", &Solver::stream_graphs_state)
       .def_property_readonly("stream_graphs_note", &Solver::stream_graphs_note)
       .def_property_readonly("ranks_per_device", &Solver::ranks_per_device)
+      .def_property_readonly("monotone_check", &Solver::monotone_check)
       .def_property_readonly("comm_transport_ranks", [](Solver& s) { return s.comm().transport_ranks(); })
       .def_property_readonly("device", [](Solver& s) { return s.backend().device(); })
       .def_property_readonly("reserved_cus", [](Solver& s) { return s.backend().reserved_cus(); })

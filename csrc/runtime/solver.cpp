@@ -437,6 +437,7 @@ Solver::~Solver() {
     }
   }
   be_->release(dstate_);
+  if (rstate_) be_->release(rstate_);
   be_->release_host(hstate_);
   comm_.reset();  // communicators before the device
 }
@@ -586,8 +587,14 @@ void Solver::initialize() {
     lean.K = K_;
     kspec2_ = lean;
   }
+  rl_ = false;
   tune_schedules();
   calibrate_remainders();
+  // the sweep form is final: its last-residual variant, where one exists
+  if (residual_last_ok()) {
+    ks_last_ = last_only(kspec2_);
+    rl_ = hip::lean_supported(dt_, ks_last_);
+  }
   reset_state();
   canary_stream_graphs();
 }
@@ -797,6 +804,15 @@ void Solver::tune_schedules() {
   if (!on || !tb_ || !be_->is_gpu()) return;
   std::vector<KernelSpec> specs{kspec2_};
   if (pick_sweep_form()) specs.push_back(pair_form());
+  // the last-residual variants of those forms: kernels of their own, whose
+  // schedules are timed (and looked up) separately
+  if (residual_last_ok()) {
+    const std::size_t nf = specs.size();
+    for (std::size_t i = 0; i < nf; ++i) {
+      const KernelSpec r = last_only(specs[i]);
+      if (hip::lean_supported(dt_, r)) specs.push_back(r);
+    }
+  }
   if ((!has_halo_ || long_halo_) && cfg_.long_sweeps && K_ + 1 <= 6 && K_ + 1 <= kResidualSlots) {
     KernelSpec ks;
     ks.kind = kspec2_.kind;
@@ -1318,10 +1334,13 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
     // one subdomain, nothing to all-reduce: the sweep's last workgroup runs
     // the check (no check kernel and its dispatch on the critical path)
     const bool fused = fused_check();
+    // full sweeps after iteration 0 (which sets the norm): the last residual
+    // only (residual_last_ok; a converging one is replayed by resolve_coarse)
+    const KernelSpec& kx = fused && rl_ && Kp == K_ && issued_ > 0 ? ks_last_ : ks;
     for (auto& l : local_) {
       StencilParams sp = params(l, dv ? l.tb_interior_long : l.tb_interior);
       sp.fuse_check = fused;
-      be_->sweep(dt_, sp, ks, kCompute);
+      be_->sweep(dt_, sp, kx, kCompute);
     }
     prof_record(prof_idx_, PE_INT1, kCompute);
     be_->range_pop();
@@ -1410,6 +1429,93 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
 bool Solver::fused_check() const {
   return cfg_.fuse_check && be_->is_gpu() && tb_ && !tb_overlap_ && local_.size() == 1 &&
          (comm_->all_local() || comm_->size() == 1) && fake_allreduce_us_ <= 0;
+}
+
+// Monotone check.  With c = 1 - 2(Dx + Dy + Dz) >= 0 the update is a convex
+// combination, T'_p = c T_p + sum_a D_a (T_{p-a} + T_{p+a}), and so is the
+// change it makes: T''_p - T'_p is the same combination of the changes T' - T
+// at p and its neighbours, which are 0 on the fixed boundary.  Hence
+// max|T'' - T'| <= max|T' - T|: the residual never grows, and a sweep whose
+// last residual is at or above the threshold has no converged step.  (In
+// floating point the residuals are those of the rounded fields; the rounding
+// moves them by ~1e-16 of the field, against a threshold-crossing step of
+// ~1e-10 of it at 1024^3, eps 1e-5.)  Converged sweeps are replayed with all
+// residuals (resolve_coarse), so conv_iter, last_residual and the fields are
+// those of the every-step check.
+bool Solver::residual_last_ok() const {
+  const double c = 1.0 - 2.0 * (phys_.D[0] + phys_.D[1] + phys_.D[2]);
+  return cfg_.monotone_check && fused_check() && cfg_.verbose <= 0 && c >= 0.0;
+}
+
+KernelSpec Solver::last_only(const KernelSpec& ks) const {
+  KernelSpec r = ks.resolved(dt_);
+  r.O = (r.O > 0 ? r.O : 0) | kResidualLastOnly;
+  return r;
+}
+
+void Solver::resolve_coarse() {
+  DeviceState& h = *hstate_;  // state(): a fresh copy of the device state
+  const int64_t c = h.conv_iter;
+  const int kc = (int)h.coarse;
+  const Segment* hit = nullptr;
+  for (const auto& sg : segs_)
+    if (c >= sg.start && c < sg.start + sg.len) hit = &sg;
+  HEAT3D_CHECK(hit && hit->len == kc && c == hit->start + kc - 1 && kc <= kResidualSlots,
+               "monotone check: sweep of iteration " << c << " (" << kc << " steps) not recorded");
+  if (!rstate_) rstate_ = static_cast<DeviceState*>(be_->alloc(sizeof(DeviceState)));
+  // scratch state: only the residual slots and the done flag are read
+  DeviceState z;
+  std::memset(&z, 0, sizeof(z));
+  for (auto& r : z.residual) r = kResidualInitBits;
+  be_->copy(rstate_, &z, offsetof(DeviceState, hist), CopyKind::H2D, kCompute);
+  for (auto& l : local_) {
+    StencilParams sp;
+    sp.in = l.field[hit->inbuf];
+    sp.out = l.field[nxt(hit->inbuf)];  // rewritten with the values it holds
+    sp.L = l.L;
+    sp.box = l.tb_interior;
+    for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+    sp.state = rstate_;
+    sp.slot = 0;
+    sp.cu_reserved = be_->reserved_cus();
+    auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
+      o[0] = u[0] < 0 ? -(K_ - 1) : u[0];
+      o[1] = u[1] > n ? n + K_ - 1 : u[1];
+    };
+    shrink(l.ux, l.sd.n[0], sp.ux);
+    shrink(l.uy, l.sd.n[1], sp.uy);
+    shrink(l.uz, l.sd.n[2], sp.uz);
+    be_->sweep(dt_, sp, kspec2_, kCompute);
+  }
+  unsigned long long bits[kResidualSlots];
+  be_->copy(bits, rstate_->residual, sizeof(unsigned long long) * kc, CopyKind::D2H, kCompute);
+  be_->sync(kCompute);
+  bool found = false;
+  for (int j = 0; j < kc && !found; ++j) {
+    const double r = __builtin_bit_cast(double, bits[j]);
+    const int64_t t = hit->start + j;
+    if (!(r == r) || r > 1.7976931348623157e308) {  // as check_convergence_scalar
+      h.fault = 1;
+      found = true;
+    } else if (r / h.norm < h.eps) {
+      found = true;
+    }
+    if (found) {
+      h.conv_iter = t;
+      h.last_residual = r;
+    }
+  }
+  HEAT3D_CHECK(found, "monotone check: the replayed sweep of iterations " << hit->start << ".." << c
+                                                                          << " has no converged step");
+  H3D_TRACE("monotone check: sweep " << hit->start << ".." << c << " converged at " << h.conv_iter);
+  h.coarse = 0;
+  // the resolved fields back to the device state (done stays set)
+  char* d = reinterpret_cast<char*>(dstate_);
+  be_->copy(d + offsetof(DeviceState, last_residual), &h.last_residual, sizeof(double), CopyKind::H2D, kCompute);
+  be_->copy(d + offsetof(DeviceState, conv_iter), &h.conv_iter, sizeof(int64_t), CopyKind::H2D, kCompute);
+  be_->copy(d + offsetof(DeviceState, fault), &h.fault, sizeof(int32_t), CopyKind::H2D, kCompute);
+  be_->copy(d + offsetof(DeviceState, coarse), &h.coarse, sizeof(uint32_t), CopyKind::H2D, kCompute);
+  be_->sync(kCompute);
 }
 
 void Solver::reduce_and_check(StreamId s, int slot0, int Kp, int prof) {
@@ -1665,7 +1771,7 @@ Solver::GraphEntry* Solver::find_graph(int G) {
   const int kind = tb_ ? 2 : 1;
   for (auto& g : graphs_)
     if (g.exec && g.G == G && g.kind == kind && g.buf == cur() && g.parity == (int)(issued_ & 1) &&
-        g.sparity == (int)(nsweep_ & 1))
+        g.sparity == (int)(nsweep_ & 1) && g.first == (issued_ == 0))
       return &g;
   return nullptr;
 }
@@ -1693,6 +1799,7 @@ Solver::GraphEntry* Solver::build_graph(int G) {
   e.buf = cur();
   e.parity = (int)(issued_ & 1);
   e.sparity = (int)(nsweep_ & 1);
+  e.first = issued_ == 0;
   bool saved[EV_COUNT];
   std::memcpy(saved, ev_valid_, sizeof(saved));
   Event saved_cur[EV_COUNT];
@@ -1858,6 +1965,7 @@ HostState Solver::state() {
   be_->sync_all();
   be_->copy(hstate_, dstate_, sizeof(DeviceState), CopyKind::D2H, kCompute);
   be_->sync(kCompute);
+  if (hstate_->done && hstate_->coarse) resolve_coarse();
   HostState h;
   h.norm = hstate_->norm;
   h.eps = hstate_->eps;

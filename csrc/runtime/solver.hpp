@@ -114,6 +114,8 @@ class Solver {
   const std::string& stream_graphs_note() const { return sg_note_; }
   // processes sharing this rank's GPU, as the launcher's environment tells
   int ranks_per_device() const { return ranks_per_device_; }
+  // full sweeps check convergence from their last residual (residual_last_ok)
+  bool monotone_check() const { return rl_; }
 
   // Error vs analytic steady state (heat3D.cu:1093-1106, with a true global
   // mean instead of rank-0's local value).  Uses the current field.
@@ -276,6 +278,18 @@ class Solver {
   // the non-overlapped sweep of a single-subdomain run checks convergence in
   // its last workgroup (StencilParams::fuse_check; --no-fused-check: off)
   bool fused_check() const;
+  // ... from the last residual of each full sweep (kResidualLastOnly): fused
+  // check, no residual history, and an update whose max-norm residual cannot
+  // grow (1 - 2(Dx + Dy + Dz) >= 0: T' is a convex combination of T's 7
+  // points, so max|T'' - T'| <= max|T' - T| with fixed boundary values)
+  bool residual_last_ok() const;
+  KernelSpec last_only(const KernelSpec& ks) const;
+  // a sweep with the last residual only set done: replay it with all K
+  // residuals (same fields, rewritten bit for bit) into a scratch state and
+  // put the first converged (or faulted) iteration into the device state
+  void resolve_coarse();
+  bool rl_ = false;                 // full sweeps run ks_last_ (residual_last_ok and the variant exists)
+  KernelSpec ks_last_;
   // lagged overlapped sweeps: the all-reduce of sweep q is issued after the
   // halo of sweep q+1 (see enqueue_multi); flush issues a pending one
   void flush_pending_reduce();
@@ -301,6 +315,7 @@ class Solver {
   struct GraphEntry {
     void* exec = nullptr;
     int G = 0, kind = 1, buf = 0, parity = 0, sparity = 0;
+    bool first = false;  // captured at iteration 0 (its first sweep computes every residual)
   };
   GraphEntry* find_graph(int G);
   GraphEntry* build_graph(int G);
@@ -344,6 +359,7 @@ class Solver {
   std::size_t esize_;
 
   DeviceState* dstate_ = nullptr;   // device
+  DeviceState* rstate_ = nullptr;   // device scratch of resolve_coarse (allocated on first use)
   DeviceState* hstate_ = nullptr;   // pinned host mirror
   int64_t issued_ = 0;              // iterations enqueued so far (absolute index)
   int cur_ = 0;               // buffer holding T^{issued_}

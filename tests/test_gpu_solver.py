@@ -173,6 +173,55 @@ def test_nan_fault_detected(h3d, gpu):
     assert r["fault"] and not r["converged"]
 
 
+@pytest.mark.parametrize("n,eps,kernel2,dtype", [((33, 33, 33), 1e-5, "auto", "fp64"),
+                                                 ((33, 33, 33), 3e-4, "auto", "fp64"),
+                                                 ((33, 33, 33), 2.9e-4, "auto", "fp64"),
+                                                 ((33, 33, 33), 2.8e-4, "auto", "fp64"),
+                                                 ((65, 47, 130), 1e-4, "tl3:1:3:1:16:0:3:2", "fp64"),
+                                                 ((65, 47, 130), 1e-4, "tl3:2:4:1:8:0:3:2", "fp64"),
+                                                 ((64, 64, 64), 1e-4, "auto", "fp32")])
+def test_monotone_check_bitwise(h3d, gpu, n, eps, kernel2, dtype):
+    """Full sweeps after iteration 0 compute only their last step's residual
+    (kResidualLastOnly; the FTCS residual max-norm never grows) and the sweep
+    that converges is replayed with all of them (Solver::resolve_coarse): the
+    same stopping iteration, last residual, norm and field, bit for bit, as
+    every step's residual (--no-monotone-check), wherever in its sweep the
+    converged step falls."""
+    kw = dict(backend="hip", dtype=dtype, extra_args=["--kernel2", kernel2])
+    a = h3d.HeatSolver(n, 10 ** 6, eps, **kw)
+    b = h3d.HeatSolver(n, 10 ** 6, eps, **dict(kw, extra_args=kw["extra_args"] + ["--no-monotone-check"]))
+    a.initialize()
+    b.initialize()
+    assert a.native.monotone_check and not b.native.monotone_check
+    ra, rb = a.run(), b.run()
+    assert ra["converged"] and ra["conv_iter"] == rb["conv_iter"], (ra, rb)
+    assert ra["last_residual"] == rb["last_residual"] and ra["norm"] == rb["norm"]
+    assert np.array_equal(a.gather(), b.gather())
+    # step() callers read the resolved iteration through state() too
+    for s in (a, b):
+        s.initialize()
+        s.step(ra["conv_iter"] + 7)
+        s.synchronize()
+    sa, sb = a.state(), b.state()
+    assert sa["conv_iter"] == sb["conv_iter"] == ra["conv_iter"] and sa["done"] == sb["done"] == 1, (sa, sb)
+    assert sa["last_residual"] == sb["last_residual"] and sa["iter"] == sb["iter"]
+    assert np.array_equal(a.gather(), b.gather())
+
+
+def test_monotone_check_nan_fault_iteration(h3d, gpu):
+    """A NaN that appears inside a last-residual-only sweep is attributed to
+    the iteration the every-step check names (the replay finds it)."""
+    res = []
+    for extra in ([], ["--no-monotone-check"]):
+        s = h3d.HeatSolver((21, 21, 21), 1000, 1e-9, backend="hip", extra_args=extra)
+        s.initialize()
+        s.step(12)
+        s.synchronize()
+        s.native.inject(0, 5, 5, 5, float("nan"))
+        res.append(s.run())
+    assert res[0]["fault"] and res[1]["fault"] and res[0]["conv_iter"] == res[1]["conv_iter"], res
+
+
 @pytest.mark.parametrize("vr", [1, 2])
 def test_schedule_autotune_bitwise(h3d, gpu, vr):
     """Start-up timing of the interior sweeps' x schedules (Solver::tune_schedules,
