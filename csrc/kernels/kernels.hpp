@@ -142,7 +142,7 @@ void pack_box(DType t, const void* f, const Layout& L, const Box& b, void* buf, 
 void unpack_box(DType t, void* f, const Layout& L, const Box& b, const void* buf, void* stream);
 void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* dst,
               const Layout& Ld, const Box& bd, void* stream);
-void check_convergence(DeviceState* s, int slot, void* stream, int count = 1);
+void check_convergence(DeviceState* s, int slot, void* stream, int count = 1, bool last_only = false);
 // kernel of `blocks` one-wave workgroups spinning for `us` microseconds on the
 // 100 MHz real-time clock (each holds a wave slot of one CU while it spins)
 // fat: in RCCL's device-kernel footprint (256 threads, 140 VGPRs, 20 KB LDS)

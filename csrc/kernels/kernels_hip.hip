@@ -777,18 +777,26 @@ void copy_box(DType t, const void* src, const Layout& Ls, const Box& bs, void* d
 }
 
 // ---- convergence check (single lane) ------------------------------------------
-__global__ void check_kernel(DeviceState* s, int slot, int count) {
+// last_only: the sweep's interior computed only its last residual (the
+// monotone check, fused_check_tail): the other slots only advance the count
+__global__ void check_kernel(DeviceState* s, int slot, int count, int last_only) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   for (int i = slot; i < slot + count; ++i) {
     const double r = __builtin_bit_cast(double, (long long)s->residual[i]);
-    check_convergence_scalar(s, r);
     s->residual[i] = kResidualInitBits;
+    if (last_only && i < slot + count - 1) {
+      s->iter = s->iter + 1;
+      continue;
+    }
+    const int was = s->done;
+    check_convergence_scalar(s, r);
+    if (last_only && !was && s->done) s->coarse = (uint32_t)count;
   }
 }
 
-void check_convergence(DeviceState* s, int slot, void* stream, int count) {
+void check_convergence(DeviceState* s, int slot, void* stream, int count, bool last_only) {
   HEAT3D_CHECK(slot >= 0 && count >= 1 && slot + count <= kResidualSlots, "residual slots " << slot << "+" << count);
-  hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, S(stream), s, slot, count);
+  hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, S(stream), s, slot, count, last_only ? 1 : 0);
   HIPK_CHECK(hipGetLastError());
 }
 

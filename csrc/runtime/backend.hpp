@@ -106,7 +106,8 @@ class Backend {
                         const Layout& Ld, const Box& bd, StreamId s) = 0;
   // convergence checks of `count` consecutive iterations, residual slots
   // slot .. slot + count - 1, in order (one launch on the GPU)
-  virtual void check_convergence(DeviceState* st, int slot, StreamId s, int count = 1) = 0;
+  // last_only: every slot but the last only advances the count (Solver::residual_last_ok)
+  virtual void check_convergence(DeviceState* st, int slot, StreamId s, int count = 1, bool last_only = false) = 0;
   virtual void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
                                 const int64_t gstart[3], double hy, DeviceState* st,
                                 StreamId s) = 0;

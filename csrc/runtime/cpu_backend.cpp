@@ -97,7 +97,8 @@ class CpuBackend final : public Backend {
                 const Layout& Ld, const Box& bd, StreamId) override {
     cpu::copy_box(t, src, Ls, bs, dst, Ld, bd);
   }
-  void check_convergence(DeviceState* st, int slot, StreamId, int count) override {
+  void check_convergence(DeviceState* st, int slot, StreamId, int count, bool last_only) override {
+    HEAT3D_CHECK(!last_only, "cpu backend: no last-residual sweeps");
     for (int i = 0; i < count; ++i) cpu::check_convergence(st, slot + i);
   }
   void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,

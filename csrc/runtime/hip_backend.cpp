@@ -481,8 +481,8 @@ class HipBackend final : public Backend {
   void delay_since(const void* slot, double us, StreamId s, int blocks) override {
     op(s, [&](hipStream_t st) { hip::delay_since(slot, us, st, blocks, fat_comm_); });
   }
-  void check_convergence(DeviceState* st, int slot, StreamId s, int count) override {
-    op(s, [&](hipStream_t q) { hip::check_convergence(st, slot, q, count); });
+  void check_convergence(DeviceState* st, int slot, StreamId s, int count, bool last_only) override {
+    op(s, [&](hipStream_t q) { hip::check_convergence(st, slot, q, count, last_only); });
   }
   void error_accumulate(DType t, const void* f, const Layout& L, const Box& box,
                         const int64_t gstart[3], double hy, DeviceState* st, StreamId s) override {

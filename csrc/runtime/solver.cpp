@@ -1305,6 +1305,12 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   // partial (Kp < K) or long (Kp = K + 1) sweeps: the kernel family's default
   // variant of depth Kp, or the one the start-up timing kept
   const KernelSpec ks = spec_for_depth(Kp);
+  // full sweeps after iteration 0 (which sets the norm): the interior computes
+  // only the last residual (residual_last_ok; boundary pieces compute all of
+  // theirs, which the check ignores but the last); a converging sweep is
+  // replayed by resolve_coarse
+  const bool rl = rl_ && Kp == K_ && issued_ > 0;
+  const KernelSpec& kx = rl ? ks_last_ : ks;
   // update ranges reach Kp - 1 (not K_ - 1) points into the deep halos
   auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
     o[0] = u[0] < 0 ? -(Kp - 1) : u[0];
@@ -1334,9 +1340,6 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
     // one subdomain, nothing to all-reduce: the sweep's last workgroup runs
     // the check (no check kernel and its dispatch on the critical path)
     const bool fused = fused_check();
-    // full sweeps after iteration 0 (which sets the norm): the last residual
-    // only (residual_last_ok; a converging one is replayed by resolve_coarse)
-    const KernelSpec& kx = fused && rl_ && Kp == K_ && issued_ > 0 ? ks_last_ : ks;
     for (auto& l : local_) {
       StencilParams sp = params(l, dv ? l.tb_interior_long : l.tb_interior);
       sp.fuse_check = fused;
@@ -1345,7 +1348,7 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
     prof_record(prof_idx_, PE_INT1, kCompute);
     be_->range_pop();
     prof_record(prof_idx_, PE_RED0, kCompute);
-    if (!fused) reduce_and_check(kCompute, slot0, Kp, prof_idx_);
+    if (!fused) reduce_and_check(kCompute, slot0, Kp, prof_idx_, rl);
     prof_record(prof_idx_, PE_CHK1, kCompute);
     if (!capturing_) {
       for (int i = 0; i < 2; ++i) {
@@ -1396,7 +1399,7 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   be_->range_push("interior");
   prof_record(prof_idx_, PE_INT0, kCompute);
   ev_wait(kCompute, EV_BND + (q ^ 1));
-  for (auto& l : local_) be_->sweep(dt_, params(l, lb ? l.tb_interior_long : l.tb_interior), ks, kCompute);
+  for (auto& l : local_) be_->sweep(dt_, params(l, lb ? l.tb_interior_long : l.tb_interior), kx, kCompute);
   prof_record(prof_idx_, PE_INT1, kCompute);
   be_->range_pop();
   ev_record(EV_INT + q, kCompute);
@@ -1422,6 +1425,7 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   pending_.slot0 = slot0;
   pending_.Kp = Kp;
   pending_.prof = prof_idx_;
+  pending_.last_only = rl;
   if (!chain_) flush_pending_reduce();
   ++nsweep_;
 }
@@ -1441,10 +1445,12 @@ bool Solver::fused_check() const {
 // moves them by ~1e-16 of the field, against a threshold-crossing step of
 // ~1e-10 of it at 1024^3, eps 1e-5.)  Converged sweeps are replayed with all
 // residuals (resolve_coarse), so conv_iter, last_residual and the fields are
-// those of the every-step check.
+// those of the every-step check.  With more than one rank the replay
+// all-reduces its residuals: state() is then collective once a run has
+// converged in such a sweep (run() calls it on every rank).
 bool Solver::residual_last_ok() const {
   const double c = 1.0 - 2.0 * (phys_.D[0] + phys_.D[1] + phys_.D[2]);
-  return cfg_.monotone_check && fused_check() && cfg_.verbose <= 0 && c >= 0.0;
+  return cfg_.monotone_check && be_->is_gpu() && tb_ && cfg_.verbose <= 0 && c >= 0.0 && fake_allreduce_us_ <= 0;
 }
 
 KernelSpec Solver::last_only(const KernelSpec& ks) const {
@@ -1468,24 +1474,42 @@ void Solver::resolve_coarse() {
   std::memset(&z, 0, sizeof(z));
   for (auto& r : z.residual) r = kResidualInitBits;
   be_->copy(rstate_, &z, offsetof(DeviceState, hist), CopyKind::H2D, kCompute);
+  // every piece of the sweep (interior, and the boundary slabs of overlapped
+  // schedules) from its input buffer, which still holds T^start and its deep
+  // halo (as finalize_converged relies on); the kernel family's default
+  // variant of depth K (every variant computes the same bits)
+  KernelSpec kd;
+  kd.kind = kspec2_.kind;
+  kd.K = K_;
   for (auto& l : local_) {
-    StencilParams sp;
-    sp.in = l.field[hit->inbuf];
-    sp.out = l.field[nxt(hit->inbuf)];  // rewritten with the values it holds
-    sp.L = l.L;
-    sp.box = l.tb_interior;
-    for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
-    sp.state = rstate_;
-    sp.slot = 0;
-    sp.cu_reserved = be_->reserved_cus();
-    auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
-      o[0] = u[0] < 0 ? -(K_ - 1) : u[0];
-      o[1] = u[1] > n ? n + K_ - 1 : u[1];
-    };
-    shrink(l.ux, l.sd.n[0], sp.ux);
-    shrink(l.uy, l.sd.n[1], sp.uy);
-    shrink(l.uz, l.sd.n[2], sp.uz);
-    be_->sweep(dt_, sp, kspec2_, kCompute);
+    std::vector<Box> pieces{l.tb_interior};
+    if (tb_overlap_) pieces.insert(pieces.end(), l.tb_boundary.begin(), l.tb_boundary.end());
+    for (std::size_t i = 0; i < pieces.size(); ++i) {
+      const Box& b = pieces[i];
+      if (b.empty()) continue;
+      StencilParams sp;
+      sp.in = l.field[hit->inbuf];
+      sp.out = l.field[nxt(hit->inbuf)];  // rewritten with the values it holds
+      sp.L = l.L;
+      sp.box = b;
+      for (int a = 0; a < 3; ++a) sp.D[a] = phys_.D[a];
+      sp.state = rstate_;
+      sp.slot = 0;
+      sp.cu_reserved = be_->reserved_cus();
+      auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
+        o[0] = u[0] < 0 ? -(K_ - 1) : u[0];
+        o[1] = u[1] > n ? n + K_ - 1 : u[1];
+      };
+      shrink(l.ux, l.sd.n[0], sp.ux);
+      shrink(l.uy, l.sd.n[1], sp.uy);
+      shrink(l.uz, l.sd.n[2], sp.uz);
+      be_->sweep(dt_, sp, i == 0 ? kspec2_ : kd, kCompute);
+    }
+  }
+  if (!comm_->all_local() && comm_->size() > 1) {
+    comm_token_wait(kCompute);
+    comm_->allreduce(rstate_->residual, kc, RedType::U64, RedOp::Max, *be_, kCompute);
+    comm_token_signal(kCompute);
   }
   unsigned long long bits[kResidualSlots];
   be_->copy(bits, rstate_->residual, sizeof(unsigned long long) * kc, CopyKind::D2H, kCompute);
@@ -1518,7 +1542,7 @@ void Solver::resolve_coarse() {
   be_->sync(kCompute);
 }
 
-void Solver::reduce_and_check(StreamId s, int slot0, int Kp, int prof) {
+void Solver::reduce_and_check(StreamId s, int slot0, int Kp, int prof, bool last_only) {
   if (!comm_->all_local() && comm_->size() > 1) {
     comm_token_wait(s);
     comm_->allreduce(&dstate_->residual[slot0], Kp, RedType::U64, RedOp::Max, *be_, s);
@@ -1527,7 +1551,7 @@ void Solver::reduce_and_check(StreamId s, int slot0, int Kp, int prof) {
     be_->delay(fake_allreduce_us_, s);  // single-GPU stand-in for the RCCL latency
   }
   prof_record(prof, PE_REDX, s);
-  be_->check_convergence(dstate_, slot0, s, Kp);
+  be_->check_convergence(dstate_, slot0, s, Kp, last_only);
 }
 
 void Solver::flush_pending_reduce() {
@@ -1538,7 +1562,7 @@ void Solver::flush_pending_reduce() {
   ev_wait(sr, EV_INT + q);
   ev_wait(sr, EV_BND + q);
   prof_record(pending_.prof, PE_RED0, sr);
-  reduce_and_check(sr, pending_.slot0, pending_.Kp, pending_.prof);
+  reduce_and_check(sr, pending_.slot0, pending_.Kp, pending_.prof, pending_.last_only);
   prof_record(pending_.prof, PE_CHK1, sr);
   ev_record(EV_CHK + q, sr);
 }

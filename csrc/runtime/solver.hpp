@@ -274,7 +274,7 @@ class Solver {
   void comm_token_wait(StreamId s);
   void comm_token_signal(StreamId s);
   // all-reduce + check of one sweep (residual slots slot0 .. slot0+Kp-1)
-  void reduce_and_check(StreamId s, int slot0, int Kp, int prof = -1);
+  void reduce_and_check(StreamId s, int slot0, int Kp, int prof = -1, bool last_only = false);
   // the non-overlapped sweep of a single-subdomain run checks convergence in
   // its last workgroup (StencilParams::fuse_check; --no-fused-check: off)
   bool fused_check() const;
@@ -392,6 +392,7 @@ class Solver {
     bool valid = false;
     int q = 0, slot0 = 0, Kp = 0;
     int prof = -1;  // profiled sweep index (profile_sweeps)
+    bool last_only = false;  // the interior computed only the last residual
   } pending_;
   Event ev_[EV_COUNT] = {};
   Event cur_ev_[EV_COUNT] = {};     // event currently standing for each id

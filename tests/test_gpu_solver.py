@@ -179,7 +179,10 @@ def test_nan_fault_detected(h3d, gpu):
                                                  ((33, 33, 33), 2.8e-4, "auto", "fp64"),
                                                  ((65, 47, 130), 1e-4, "tl3:1:3:1:16:0:3:2", "fp64"),
                                                  ((65, 47, 130), 1e-4, "tl3:2:4:1:8:0:3:2", "fp64"),
-                                                 ((64, 64, 64), 1e-4, "auto", "fp32")])
+                                                 ((64, 64, 64), 1e-4, "auto", "fp32"),
+                                                 ((67, 45, 131), 1e-4, "vr3", "fp64"),
+                                                 ((40, 44, 48), 3e-4, "vr2x2", "fp64"),
+                                                 ((67, 45, 131), 1e-4, "vr3-nolag", "fp32")])
 def test_monotone_check_bitwise(h3d, gpu, n, eps, kernel2, dtype):
     """Full sweeps after iteration 0 compute only their last step's residual
     (kResidualLastOnly; the FTCS residual max-norm never grows) and the sweep
@@ -187,7 +190,15 @@ def test_monotone_check_bitwise(h3d, gpu, n, eps, kernel2, dtype):
     same stopping iteration, last residual, norm and field, bit for bit, as
     every step's residual (--no-monotone-check), wherever in its sweep the
     converged step falls."""
-    kw = dict(backend="hip", dtype=dtype, extra_args=["--kernel2", kernel2])
+    # vr*: virtual ranks (overlapped slabs / blocks: the check kernel after the
+    # all-reduce, interior last-residual-only, boundary slabs every residual)
+    if kernel2.startswith("vr"):
+        decomp = {"vr3": (3, 1, 1), "vr2x2": (1, 2, 2), "vr3-nolag": (3, 1, 1)}[kernel2]
+        extra = ["--lag", "off"] if kernel2.endswith("nolag") else []
+        kw = dict(backend="hip", dtype=dtype, virtual_ranks=decomp[0] * decomp[1] * decomp[2], decomp=decomp,
+                  extra_args=extra)
+    else:
+        kw = dict(backend="hip", dtype=dtype, extra_args=["--kernel2", kernel2])
     a = h3d.HeatSolver(n, 10 ** 6, eps, **kw)
     b = h3d.HeatSolver(n, 10 ** 6, eps, **dict(kw, extra_args=kw["extra_args"] + ["--no-monotone-check"]))
     a.initialize()
