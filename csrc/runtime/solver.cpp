@@ -953,26 +953,37 @@ void Solver::calibrate_remainders() {
     int Kp;
     KernelSpec ks;
     std::string name;
+    KernelSpec form;  // depth K_: the sweep form the candidate times (its last-residual variant may run)
   };
-  std::vector<Cand> cands{{K_, kspec2_, "sweep" + std::to_string(K_)},
-                          {K_ + 1, spec_for_depth(K_ + 1), "sweep" + std::to_string(K_ + 1)}};
+  // full sweeps after iteration 0 run a form's last-residual variant where
+  // the monotone check is on: the forms are timed (and compared) as they run
+  const bool rl_forms = residual_last_ok();
+  auto as_run = [&](const KernelSpec& f) {
+    if (!rl_forms) return f;
+    const KernelSpec r = last_only(f);
+    return hip::lean_supported(dt_, r) ? r : f;
+  };
+  std::vector<Cand> cands{{K_, as_run(kspec2_), "sweep" + std::to_string(K_), kspec2_},
+                          {K_ + 1, spec_for_depth(K_ + 1), "sweep" + std::to_string(K_ + 1), {}}};
   const bool pick_form = pick_sweep_form();
   if (pick_form) {
-    cands.push_back({K_, pair_form(), "sweep" + std::to_string(K_) + "[" + pair_form().resolved(dt_).str() + "]"});
+    const KernelSpec pr = as_run(pair_form());
+    cands.push_back({K_, pr, "sweep" + std::to_string(K_) + "[" + pr.resolved(dt_).str() + "]", pair_form()});
     KernelSpec pl = pair_form();  // and the pair form of the long sweep
     pl.K = K_ + 1;
     if (hip::lean_supported(dt_, pl))
-      cands.push_back({K_ + 1, pl, "sweep" + std::to_string(K_ + 1) + "[" + pl.resolved(dt_).str() + "]"});
+      cands.push_back({K_ + 1, pl, "sweep" + std::to_string(K_ + 1) + "[" + pl.resolved(dt_).str() + "]", {}});
   }
   for (int r = 1; r < K_; ++r) {
     if (r == 2 && dt_ == DType::F64 && kspec2_.kind == KernelSpec::TBL && be_->is_gpu()) {
       for (const char* v : {"tl2:1:5:1:16:0:3:2", "tl2:1:3:1:16:0:3:2", "tl2:2:6:1:8:0:3:2"}) {
         const KernelSpec ks = KernelSpec::parse(v);
-        if (hip::lean_supported(dt_, ks)) cands.push_back({2, ks, std::string("sweep2[") + v + "]"});
+        if (hip::lean_supported(dt_, ks)) cands.push_back({2, ks, std::string("sweep2[") + v + "]", {}});
       }
       continue;
     }
-    cands.push_back({r, r == 1 ? kspec_ : spec_for_depth(r), r == 1 ? std::string("step") : "sweep" + std::to_string(r)});
+    cands.push_back(
+        {r, r == 1 ? kspec_ : spec_for_depth(r), r == 1 ? std::string("step") : "sweep" + std::to_string(r), {}});
   }
   // the GPU is cold here (initialisation, no sweeps yet): keep it busy with
   // regular sweeps for >= 30 ms before timing, then take the best of two
@@ -1009,7 +1020,7 @@ void Solver::calibrate_remainders() {
         depth_spec_[Kp] = cands[c].ks;
         depth_set_[Kp] = true;
       }
-      if (Kp == K_ && pick_form) kspec2_ = cands[c].ks;  // the faster sweep form (pick_sweep_form)
+      if (Kp == K_ && pick_form) kspec2_ = cands[c].form;  // the faster sweep form (pick_sweep_form)
     }
   }
   for (int Kp = 2; Kp < K_; ++Kp)

@@ -208,7 +208,10 @@ def test_monotone_check_bitwise(h3d, gpu, n, eps, kernel2, dtype):
     assert ra["converged"] and ra["conv_iter"] == rb["conv_iter"], (ra, rb)
     assert ra["last_residual"] == rb["last_residual"] and ra["norm"] == rb["norm"]
     assert np.array_equal(a.gather(), b.gather())
-    # step() callers read the resolved iteration through state() too
+    # step() callers read the resolved iteration through state() too.  (Their
+    # field is T at the end of the converging sweep, which depends on how the
+    # steps were cut into sweeps: the start-up timing of the two solvers may
+    # choose different remainder sweeps, so it is not compared here.)
     for s in (a, b):
         s.initialize()
         s.step(ra["conv_iter"] + 7)
@@ -216,7 +219,6 @@ def test_monotone_check_bitwise(h3d, gpu, n, eps, kernel2, dtype):
     sa, sb = a.state(), b.state()
     assert sa["conv_iter"] == sb["conv_iter"] == ra["conv_iter"] and sa["done"] == sb["done"] == 1, (sa, sb)
     assert sa["last_residual"] == sb["last_residual"] and sa["iter"] == sb["iter"]
-    assert np.array_equal(a.gather(), b.gather())
 
 
 def test_monotone_check_nan_fault_iteration(h3d, gpu):
