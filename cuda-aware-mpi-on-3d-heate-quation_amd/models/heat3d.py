@@ -196,6 +196,12 @@ class HeatSolver:
         self._s.prepare_steps(int(n))
 
     def state(self) -> Dict:
+        """Convergence state (iter, conv_iter, done, fault, norm, last_residual, ...).
+
+        With the monotone check (Solver::resolve_coarse) the first call after a
+        multi-rank run converged inside a sweep that computed only its last
+        residual replays that sweep and all-reduces its residuals: call it on
+        every rank then (``run()`` already does)."""
         return dict(self._s.state())
 
     # -- data ------------------------------------------------------------------
