@@ -212,6 +212,11 @@ int main(int argc, char** argv) {
     if (rank_from_env() == 0) {
       std::cout << Config::usage() << std::flush;
       std::cerr << "heat3d: " << e.what() << std::endl;
+    } else {
+      // a launcher (mpirun) tears the job down at the first failed rank: give
+      // rank 0's usage text time to be written and forwarded first (without
+      // this pause mpirun lost it now and then: tests/test_mpirun_cli.py)
+      std::this_thread::sleep_for(std::chrono::milliseconds(500));
     }
     return 1;
   }
