@@ -117,6 +117,9 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
   H3D_TBLA(3, 16, 3, 2) H3D_TBLA(3, 16, 3, 3) H3D_TBLA(3, 16, 3, 17)
   H3D_TBLA(3, 16, 3, 18) H3D_TBLA(3, 16, 3, 19)
   H3D_TBLA(3, 16, 3, 2 | kResidualLastOnly)  // fp64 / fp32 K = 3 default, last residual only
+  // ... and the partial / long sweeps' shapes (K = 2 candidates, the K = 4 default)
+  H3D_TBLA(3, 16, 2, 2 | kResidualLastOnly) H3D_TBLA(5, 16, 2, 2 | kResidualLastOnly)
+  H3D_TBLA(3, 12, 4, 2 | kResidualLastOnly)
   H3D_TBLA(2, 16, 4, 2) H3D_TBLA(3, 16, 2, 2) H3D_TBLA(5, 16, 2, 2)
   H3D_TBLA(3, 12, 4, 2)  // the fp64 K = 4 default (long sweeps: 12 waves, 36 rows)
   H3D_TBLA(4, 12, 4, 2)

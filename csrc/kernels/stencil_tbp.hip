@@ -548,7 +548,8 @@ static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) 
     // LDS), K = 2 in 6 rows and K = 4 in 3 rows of 8 waves; nt stores (2) or
     // default (0)
     H3D_TBP(4, 8, 3, 3, 2) H3D_TBP(4, 8, 3, 3, 0) H3D_TBP(6, 8, 2, 3, 2)
-    H3D_TBP(4, 8, 3, 3, 2 | kResidualLastOnly)
+    H3D_TBP(4, 8, 3, 3, 2 | kResidualLastOnly) H3D_TBP(6, 8, 2, 3, 2 | kResidualLastOnly)
+    H3D_TBP(3, 8, 4, 3, 2 | kResidualLastOnly)
     H3D_TBP(3, 8, 4, 3, 2)
   }
 #undef H3D_TBP

@@ -588,13 +588,17 @@ void Solver::initialize() {
     kspec2_ = lean;
   }
   rl_ = false;
+  for (bool& b : rl_d_) b = false;
   tune_schedules();
   calibrate_remainders();
   // the sweep form is final: its last-residual variant, where one exists
-  if (residual_last_ok()) {
-    ks_last_ = last_only(kspec2_);
-    rl_ = hip::lean_supported(dt_, ks_last_);
-  }
+  // the sweep shapes are final: their last-residual variants, where they exist
+  if (residual_last_ok())
+    for (int Kp = 2; Kp <= K_ + 1 && Kp < 8; ++Kp) {
+      ks_last_[Kp] = last_only(spec_for_depth(Kp));
+      rl_d_[Kp] = hip::lean_supported(dt_, ks_last_[Kp]);
+    }
+  rl_ = rl_d_[K_];
   reset_state();
   canary_stream_graphs();
 }
@@ -804,7 +808,13 @@ void Solver::tune_schedules() {
   if (!on || !tb_ || !be_->is_gpu()) return;
   std::vector<KernelSpec> specs{kspec2_};
   if (pick_sweep_form()) specs.push_back(pair_form());
-  // the last-residual variants of those forms: kernels of their own, whose
+  if ((!has_halo_ || long_halo_) && cfg_.long_sweeps && K_ + 1 <= 6 && K_ + 1 <= kResidualSlots) {
+    KernelSpec ks;
+    ks.kind = kspec2_.kind;
+    ks.K = K_ + 1;
+    if (hip::lean_supported(dt_, ks)) specs.push_back(ks);
+  }
+  // the last-residual variants of those: kernels of their own, whose
   // schedules are timed (and looked up) separately
   if (residual_last_ok()) {
     const std::size_t nf = specs.size();
@@ -812,12 +822,6 @@ void Solver::tune_schedules() {
       const KernelSpec r = last_only(specs[i]);
       if (hip::lean_supported(dt_, r)) specs.push_back(r);
     }
-  }
-  if ((!has_halo_ || long_halo_) && cfg_.long_sweeps && K_ + 1 <= 6 && K_ + 1 <= kResidualSlots) {
-    KernelSpec ks;
-    ks.kind = kspec2_.kind;
-    ks.K = K_ + 1;
-    if (hip::lean_supported(dt_, ks)) specs.push_back(ks);
   }
   for (const KernelSpec& ks : specs) {
     const int Kp = ks.K;
@@ -953,10 +957,10 @@ void Solver::calibrate_remainders() {
     int Kp;
     KernelSpec ks;
     std::string name;
-    KernelSpec form;  // depth K_: the sweep form the candidate times (its last-residual variant may run)
+    KernelSpec form;  // the sweep shape the candidate stands for (it times the variant that runs)
   };
-  // full sweeps after iteration 0 run a form's last-residual variant where
-  // the monotone check is on: the forms are timed (and compared) as they run
+  // sweeps after iteration 0 run a shape's last-residual variant where the
+  // monotone check is on: the shapes are timed (and compared) as they run
   const bool rl_forms = residual_last_ok();
   auto as_run = [&](const KernelSpec& f) {
     if (!rl_forms) return f;
@@ -964,7 +968,8 @@ void Solver::calibrate_remainders() {
     return hip::lean_supported(dt_, r) ? r : f;
   };
   std::vector<Cand> cands{{K_, as_run(kspec2_), "sweep" + std::to_string(K_), kspec2_},
-                          {K_ + 1, spec_for_depth(K_ + 1), "sweep" + std::to_string(K_ + 1), {}}};
+                          {K_ + 1, as_run(spec_for_depth(K_ + 1)), "sweep" + std::to_string(K_ + 1),
+                           spec_for_depth(K_ + 1)}};
   const bool pick_form = pick_sweep_form();
   if (pick_form) {
     const KernelSpec pr = as_run(pair_form());
@@ -972,18 +977,18 @@ void Solver::calibrate_remainders() {
     KernelSpec pl = pair_form();  // and the pair form of the long sweep
     pl.K = K_ + 1;
     if (hip::lean_supported(dt_, pl))
-      cands.push_back({K_ + 1, pl, "sweep" + std::to_string(K_ + 1) + "[" + pl.resolved(dt_).str() + "]", {}});
+      cands.push_back({K_ + 1, as_run(pl), "sweep" + std::to_string(K_ + 1) + "[" + pl.resolved(dt_).str() + "]", pl});
   }
   for (int r = 1; r < K_; ++r) {
     if (r == 2 && dt_ == DType::F64 && kspec2_.kind == KernelSpec::TBL && be_->is_gpu()) {
       for (const char* v : {"tl2:1:5:1:16:0:3:2", "tl2:1:3:1:16:0:3:2", "tl2:2:6:1:8:0:3:2"}) {
         const KernelSpec ks = KernelSpec::parse(v);
-        if (hip::lean_supported(dt_, ks)) cands.push_back({2, ks, std::string("sweep2[") + v + "]", {}});
+        if (hip::lean_supported(dt_, ks)) cands.push_back({2, as_run(ks), std::string("sweep2[") + v + "]", ks});
       }
       continue;
     }
-    cands.push_back(
-        {r, r == 1 ? kspec_ : spec_for_depth(r), r == 1 ? std::string("step") : "sweep" + std::to_string(r), {}});
+    const KernelSpec base = r == 1 ? kspec_ : spec_for_depth(r);
+    cands.push_back({r, r == 1 ? base : as_run(base), r == 1 ? std::string("step") : "sweep" + std::to_string(r), base});
   }
   // the GPU is cold here (initialisation, no sweeps yet): keep it busy with
   // regular sweeps for >= 30 ms before timing, then take the best of two
@@ -1017,7 +1022,7 @@ void Solver::calibrate_remainders() {
     if (best[c] < cost[Kp]) {
       cost[Kp] = best[c];
       if (Kp != K_ && Kp > 1) {
-        depth_spec_[Kp] = cands[c].ks;
+        depth_spec_[Kp] = cands[c].form;
         depth_set_[Kp] = true;
       }
       if (Kp == K_ && pick_form) kspec2_ = cands[c].form;  // the faster sweep form (pick_sweep_form)
@@ -1316,12 +1321,12 @@ void Solver::enqueue_multi(int bi, int Kp, bool thick) {
   // partial (Kp < K) or long (Kp = K + 1) sweeps: the kernel family's default
   // variant of depth Kp, or the one the start-up timing kept
   const KernelSpec ks = spec_for_depth(Kp);
-  // full sweeps after iteration 0 (which sets the norm): the interior computes
+  // sweeps after iteration 0 (which sets the norm): the interior computes
   // only the last residual (residual_last_ok; boundary pieces compute all of
   // theirs, which the check ignores but the last); a converging sweep is
   // replayed by resolve_coarse
-  const bool rl = rl_ && Kp == K_ && issued_ > 0;
-  const KernelSpec& kx = rl ? ks_last_ : ks;
+  const bool rl = Kp >= 2 && Kp < 8 && rl_d_[Kp] && issued_ > 0;
+  const KernelSpec& kx = rl ? ks_last_[Kp] : ks;
   // update ranges reach Kp - 1 (not K_ - 1) points into the deep halos
   auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
     o[0] = u[0] < 0 ? -(Kp - 1) : u[0];
@@ -1487,14 +1492,19 @@ void Solver::resolve_coarse() {
   be_->copy(rstate_, &z, offsetof(DeviceState, hist), CopyKind::H2D, kCompute);
   // every piece of the sweep (interior, and the boundary slabs of overlapped
   // schedules) from its input buffer, which still holds T^start and its deep
-  // halo (as finalize_converged relies on); the kernel family's default
-  // variant of depth K (every variant computes the same bits)
+  // halo (as finalize_converged relies on); the interior in the sweep's shape,
+  // the boundary pieces in the kernel family's default variant of its depth
+  // (every variant computes the same bits)
   KernelSpec kd;
   kd.kind = kspec2_.kind;
-  kd.K = K_;
+  kd.K = kc;
+  const bool lng = kc > K_;
   for (auto& l : local_) {
-    std::vector<Box> pieces{l.tb_interior};
-    if (tb_overlap_) pieces.insert(pieces.end(), l.tb_boundary.begin(), l.tb_boundary.end());
+    std::vector<Box> pieces{lng ? l.tb_interior_long : l.tb_interior};
+    if (tb_overlap_) {
+      const std::vector<Box>& bnd = lng ? l.tb_boundary_long : l.tb_boundary;
+      pieces.insert(pieces.end(), bnd.begin(), bnd.end());
+    }
     for (std::size_t i = 0; i < pieces.size(); ++i) {
       const Box& b = pieces[i];
       if (b.empty()) continue;
@@ -1508,13 +1518,13 @@ void Solver::resolve_coarse() {
       sp.slot = 0;
       sp.cu_reserved = be_->reserved_cus();
       auto shrink = [&](const int64_t (&u)[2], int64_t n, int64_t (&o)[2]) {
-        o[0] = u[0] < 0 ? -(K_ - 1) : u[0];
-        o[1] = u[1] > n ? n + K_ - 1 : u[1];
+        o[0] = u[0] < 0 ? -(kc - 1) : u[0];
+        o[1] = u[1] > n ? n + kc - 1 : u[1];
       };
       shrink(l.ux, l.sd.n[0], sp.ux);
       shrink(l.uy, l.sd.n[1], sp.uy);
       shrink(l.uz, l.sd.n[2], sp.uz);
-      be_->sweep(dt_, sp, i == 0 ? kspec2_ : kd, kCompute);
+      be_->sweep(dt_, sp, i == 0 ? spec_for_depth(kc) : kd, kCompute);
     }
   }
   if (!comm_->all_local() && comm_->size() > 1) {

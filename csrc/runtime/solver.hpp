@@ -288,8 +288,11 @@ class Solver {
   // residuals (same fields, rewritten bit for bit) into a scratch state and
   // put the first converged (or faulted) iteration into the device state
   void resolve_coarse();
-  bool rl_ = false;                 // full sweeps run ks_last_ (residual_last_ok and the variant exists)
-  KernelSpec ks_last_;
+  // sweeps of depth Kp >= 2 after iteration 0 run ks_last_[Kp] where rl_d_[Kp]
+  // (residual_last_ok and the variant exists); rl_ = rl_d_[K_]
+  bool rl_ = false;
+  bool rl_d_[8] = {};
+  KernelSpec ks_last_[8];
   // lagged overlapped sweeps: the all-reduce of sweep q is issued after the
   // halo of sweep q+1 (see enqueue_multi); flush issues a pending one
   void flush_pending_reduce();

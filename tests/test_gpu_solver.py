@@ -221,6 +221,32 @@ def test_monotone_check_bitwise(h3d, gpu, n, eps, kernel2, dtype):
     assert sa["last_residual"] == sb["last_residual"] and sa["iter"] == sb["iter"]
 
 
+@pytest.mark.parametrize("chunk", [5, 4, 7])
+@pytest.mark.parametrize("vr", [1, 3])
+def test_monotone_check_partial_and_long_sweeps(h3d, gpu, chunk, vr):
+    """step() in chunks that are not multiples of K = 3 ends every chunk in a
+    partial sweep or runs long (K+1) ones (the remainder policy): those run
+    their last-residual variants too, and a convergence inside one resolves to
+    the every-step iteration.  Several thresholds move the converged step
+    through the sweeps of the chunks."""
+    kw = dict(backend="hip", virtual_ranks=vr, decomp=(vr, 1, 1))
+    for eps in (3e-4, 2.9e-4, 2.8e-4, 2.7e-4, 2.6e-4):
+        out = []
+        for extra in ([], ["--no-monotone-check"]):
+            s = h3d.HeatSolver((33, 33, 33), 10 ** 6, eps, extra_args=extra, **kw)
+            s.initialize()
+            while True:
+                s.step(chunk)
+                s.synchronize()
+                st = s.state()
+                if st["done"]:
+                    break
+            out.append(st)
+        a, b = out
+        assert a["conv_iter"] == b["conv_iter"] and a["last_residual"] == b["last_residual"], (eps, a, b)
+        assert a["fault"] == b["fault"] == 0
+
+
 def test_monotone_check_nan_fault_iteration(h3d, gpu):
     """A NaN that appears inside a last-residual-only sweep is attributed to
     the iteration the every-step check names (the replay finds it)."""

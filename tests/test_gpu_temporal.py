@@ -106,10 +106,11 @@ def test_temporal_slabs_gpu_fixed_iters(h3d, gpu, iters):
 VARIANTS_K = {3: ["tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5:3", "tl3:1:3:1:16:0:6",
                   "tl3:1:2:1:16:7:6", "tl3:1:6:1:8:0:3", "tl3:1:3:1:16:0:3:2", "tl3:1:3:1:16:0:3:19", "tl3:1:3:1:16:0:3:0",
                   "tl3:1:3:1:16:0:3:66"],
-              4: ["tl4", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6", "tl4:1:2:1:16:5:6",
+              4: ["tl4", "tl4:1:3:1:12:0:3:66", "tl4:1:2:1:16:0:4", "tl4:1:2:1:16:7:3", "tl4:1:2:1:16:0:6",
+                  "tl4:1:2:1:16:5:6",
                   "tl4:1:6:1:8:0:3", "tl4:1:6:1:8:0:4", "tl4:1:5:1:8:0:3", "tl4:1:6:1:8:7:3",
                   "tl4:1:3:1:12:0:3:2", "tl4:1:3:1:12:0:3"],
-              2: ["tl2", "tl2:1:2:1:16:0:3", "tl2:1:5:1:16:0:3:2"]}
+              2: ["tl2", "tl2:1:2:1:16:0:3", "tl2:1:5:1:16:0:3:2", "tl2:1:5:1:16:0:3:66", "tl2:1:3:1:16:0:3:66"]}
 # fp32: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)
 PAIR = {3: ["tl3:2:3:1:16:0:3", "tl3:2:3:1:16:0:3:2", "tl3:2:3:1:16:0:3:66", "tl3:2:3:1:16:0:4", "tl3:2:2:1:16:0:3", "tl3:2:3:1:16:5:3"],
         4: ["tl4:2:2:1:16:0:3", "tl4:2:2:1:16:0:4", "tl4:2:2:1:16:7:3"],
@@ -121,11 +122,13 @@ def _last_only(kernel):
     """Spec store field bit 64: only the last step's residual is computed."""
     parts = kernel.split(":")
     return len(parts) > 7 and bool(int(parts[7]) & 64)
+
+
 # fp64: the same kernel with 16-byte pairs (8 waves; round 5)
 # (store field bit 64: the last step's residual only, the monotone check)
 PAIR_F64 = {3: ["tl3:2", "tl3:2:4:1:8:0:3:0", "tl3:2:4:1:8:5:3:2", "tl3:2:4:1:8:0:3:66", "tl3:2:4:1:8:5:3:66"],
-            4: ["tl4:2", "tl4:2:3:1:8:7:3:2"],
-            2: ["tl2:2", "tl2:2:6:1:8:0:3:2"]}
+            4: ["tl4:2", "tl4:2:3:1:8:7:3:2", "tl4:2:3:1:8:0:3:66"],
+            2: ["tl2:2", "tl2:2:6:1:8:0:3:2", "tl2:2:6:1:8:0:3:66"]}
 
 
 @pytest.mark.parametrize("K", [2, 3, 4])
@@ -599,8 +602,10 @@ def test_remainder_policy_measured_gpu(h3d, gpu, vr, dims):
     t3 = min(v for k, v in costs.items() if k.split("[")[0] == "sweep3")
     t4 = min(v for k, v in costs.items() if k.split("[")[0] == "sweep4")
     rem = a.native.long_remainders
+    # with halos a long remainder must win by 15 % (Solver::calibrate_remainders)
+    margin = 1.15 if vr > 1 else 1.0
     for r in (1, 2):
-        assert (r in rem) == (r * (t4 - t3) < costs["step" if r == 1 else "sweep2"]), (rem, costs)
+        assert (r in rem) == (r * (t4 - t3) * margin < costs["step" if r == 1 else "sweep2"]), (rem, costs)
     for k in (5, 20, 7):
         a.step(k)
         b.step(k)
