@@ -377,6 +377,7 @@ def run_rank(args) -> int:
                                     "dims": list(dims), "rccl_p2p_channels": s.native.rccl_p2p_channels or None,
                                     "subdomain": list(s.native.local_subdomain(0)["n"]), "x_schedules": xs,
                                     "long_remainders": list(s.native.long_remainders),
+                                    "long_major": bool(s.native.long_major),
                                     "sweep_costs_ms": {k: round(v, 4) for k, v in s.native.sweep_costs.items()}},
                                    group)
     # per-rank schedule profile, after (outside) the timed window: a few more

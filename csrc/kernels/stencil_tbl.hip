@@ -120,6 +120,11 @@ static bool dispatch_tbl(const StencilParams* p, const KernelSpec& k, hipStream_
   // ... and the partial / long sweeps' shapes (K = 2 candidates, the K = 4 default)
   H3D_TBLA(3, 16, 2, 2 | kResidualLastOnly) H3D_TBLA(5, 16, 2, 2 | kResidualLastOnly)
   H3D_TBLA(3, 12, 4, 2 | kResidualLastOnly)
+  if constexpr (sizeof(Real) == 8) {
+    // fp64 48-row K = 4 and 36-row K = 5 tiles of 12 waves: 167 VGPRs without
+    // the K - 1 residual maxima
+    H3D_TBLA(4, 12, 4, 2 | kResidualLastOnly) H3D_TBLA(3, 12, 5, 2 | kResidualLastOnly)
+  }
   H3D_TBLA(2, 16, 4, 2) H3D_TBLA(3, 16, 2, 2) H3D_TBLA(5, 16, 2, 2)
   H3D_TBLA(3, 12, 4, 2)  // the fp64 K = 4 default (long sweeps: 12 waves, 36 rows)
   H3D_TBLA(4, 12, 4, 2)

@@ -769,6 +769,7 @@ PYBIND11_MODULE(_heat3d, m) {
       .def_property_readonly("ghost_depth", &Solver::ghost_depth)
       .def_property_readonly("long_halo_sweeps", &Solver::long_halo_sweeps)
       .def("sweep_pieces", &Solver::sweep_pieces, py::arg("local") = 0)
+      .def_property_readonly("long_major", &Solver::long_major)
       .def_property_readonly("long_remainders",
                              [](const Solver& s) {
                                std::vector<int> r;

@@ -595,7 +595,10 @@ void Solver::initialize() {
   // the sweep shapes are final: their last-residual variants, where they exist
   if (residual_last_ok())
     for (int Kp = 2; Kp <= K_ + 1 && Kp < 8; ++Kp) {
-      ks_last_[Kp] = last_only(spec_for_depth(Kp));
+      // the timed winner where it is a last-residual variant, else the
+      // depth's shape in that form
+      const bool picked = (rl_pick_[Kp].O & kResidualLastOnly) != 0;
+      ks_last_[Kp] = picked ? rl_pick_[Kp] : last_only(spec_for_depth(Kp));
       rl_d_[Kp] = hip::lean_supported(dt_, ks_last_[Kp]);
     }
   rl_ = rl_d_[K_];
@@ -896,6 +899,8 @@ KernelSpec Solver::pair_form() const {
 }
 
 void Solver::calibrate_remainders() {
+  long_major_ = false;
+  for (auto& k : rl_pick_) k = KernelSpec{};
   long_rem_ = ~0u;
   for (bool& d : depth_set_) d = false;
   if (!tb_ || cfg_.long_sweeps == 0) {
@@ -970,6 +975,16 @@ void Solver::calibrate_remainders() {
   std::vector<Cand> cands{{K_, as_run(kspec2_), "sweep" + std::to_string(K_), kspec2_},
                           {K_ + 1, as_run(spec_for_depth(K_ + 1)), "sweep" + std::to_string(K_ + 1),
                            spec_for_depth(K_ + 1)}};
+  // fp64 K = 4 in 48-row tiles of 12 waves (167 VGPRs in the last-residual
+  // form): the fastest long sweep on one GPU (1022^3 / 510^3 kernel level 906 /
+  // 846 against 886-892 / 824 for 36-row tiles, gpurun_out/r6k4)
+  if (dt_ == DType::F64 && K_ == 3 && kspec2_.kind == KernelSpec::TBL && cfg_.kernel2 == "auto" && rl_forms) {
+    // (the every-residual form spills: iteration 0's sweep and the replay of
+    // one that converged run the default K + 1 shape)
+    const KernelSpec t = KernelSpec::parse("tl4:1:4:1:12:0:3:66");
+    if (hip::lean_supported(dt_, t))
+      cands.push_back({K_ + 1, t, "sweep" + std::to_string(K_ + 1) + "[" + t.str() + "]", spec_for_depth(K_ + 1)});
+  }
   const bool pick_form = pick_sweep_form();
   if (pick_form) {
     const KernelSpec pr = as_run(pair_form());
@@ -1021,6 +1036,7 @@ void Solver::calibrate_remainders() {
     const int Kp = cands[c].Kp;
     if (best[c] < cost[Kp]) {
       cost[Kp] = best[c];
+      if (Kp > 1 && Kp < 8) rl_pick_[Kp] = cands[c].ks;  // the variant that runs (last residual or not)
       if (Kp != K_ && Kp > 1) {
         depth_spec_[Kp] = cands[c].form;
         depth_set_[Kp] = true;
@@ -1034,6 +1050,11 @@ void Solver::calibrate_remainders() {
         }) > 1)
       sweep_costs_.push_back({"sweep" + std::to_string(Kp), cost[Kp]});
   const double tk = cost[K_], tl = cost[K_ + 1];
+  // long-major: where a K+1 sweep costs less per step than a K one (one
+  // subdomain: the last-residual K = 4 sweep at 1022^3, 4.18 against 3.29 ms
+  // for K = 3), step counts run as many long sweeps as they can
+  // (long_sweeps_for)
+  long_major_ = !has_halo_ && local_.size() == 1 && tl < 1e30 && tl / (K_ + 1) < tk / K_;
   // votes for the partial sweep, one slot per remainder; the ranks agree on
   // the max: long only where no rank found the partial sweep cheaper (the
   // halo depth of every exchange must match between neighbours)
@@ -1773,8 +1794,16 @@ int Solver::graph_len_for(int64_t n) const {
 }
 
 int Solver::long_sweeps_for(int64_t n) const {
-  if (!tb_ || (has_halo_ && !long_halo_) || !kspec2_.multi_step() || n % K_ == 0) return 0;
+  if (!tb_ || (has_halo_ && !long_halo_) || !kspec2_.multi_step()) return 0;
   if (K_ + 1 > 6 || K_ + 1 > kResidualSlots) return 0;
+  if (long_major_ && cfg_.long_sweeps) {
+    // the most long sweeps b with n - b (K + 1) a multiple of K (b = n mod K
+    // modulo K); none fits: the remainder policy below
+    const int64_t bmax = n / (K_ + 1), r = n % K_;
+    const int64_t b = bmax - (((bmax - r) % K_) + K_) % K_;
+    if (b > 0 && b * (K_ + 1) <= n && (n - b * (K_ + 1)) % K_ == 0) return (int)std::min<int64_t>(b, INT32_MAX);
+  }
+  if (n % K_ == 0) return 0;
   const int64_t b = n % K_;             // n = a K + b (K + 1) with a = (n - b (K + 1)) / K
   if (b * (K_ + 1) > n) return 0;
   if (!cfg_.long_sweeps || !((long_rem_ >> b) & 1u)) return 0;

@@ -153,6 +153,7 @@ class Solver {
   // remainder policy: which n mod K run as long sweeps, and the start-up
   // sweep timings that decided it (empty when not measured)
   unsigned long_remainders() const { return long_rem_; }
+  bool long_major() const { return long_major_; }
   const std::vector<std::pair<std::string, double>>& sweep_costs() const { return sweep_costs_; }
   // HBM preflight (constructor): bytes this solver allocates for its local
   // ranks (fields + face staging), and the backend's free / total memory
@@ -292,7 +293,9 @@ class Solver {
   // (residual_last_ok and the variant exists); rl_ = rl_d_[K_]
   bool rl_ = false;
   bool rl_d_[8] = {};
+  bool long_major_ = false;          // K+1 sweeps cheaper per step (calibrate_remainders, long_sweeps_for)
   KernelSpec ks_last_[8];
+  KernelSpec rl_pick_[8];            // per depth: the variant the start-up timing kept
   // lagged overlapped sweeps: the all-reduce of sweep q is issued after the
   // halo of sweep q+1 (see enqueue_multi); flush issues a pending one
   void flush_pending_reduce();
