@@ -1841,8 +1841,8 @@ bool Solver::stream_graphs_enabled() const {
   return true;
 }
 
-Solver::GraphEntry* Solver::find_graph(int G) {
-  const int kind = tb_ ? 2 : 1;
+Solver::GraphEntry* Solver::find_graph(int G, int kind_req) {
+  const int kind = kind_req ? kind_req : tb_ ? 2 : 1;
   for (auto& g : graphs_)
     if (g.exec && g.G == G && g.kind == kind && g.buf == cur() && g.parity == (int)(issued_ & 1) &&
         g.sparity == (int)(nsweep_ & 1) && g.first == (issued_ == 0))
@@ -1864,12 +1864,12 @@ void Solver::destroy_graphs() {
 // one linear graph per stream (the backend forks and joins the streams around
 // their launch).  The solver's host-side schedule state is restored
 // afterwards: a launch advances it exactly like the eager path.
-Solver::GraphEntry* Solver::build_graph(int G) {
-  H3D_TRACE("build_graph G=" << G << " at issued=" << issued_);
+Solver::GraphEntry* Solver::build_graph(int G, int kind_req) {
+  H3D_TRACE("build_graph G=" << G << " kind " << kind_req << " at issued=" << issued_);
   join_pipeline();
   GraphEntry e;
   e.G = G;
-  e.kind = tb_ ? 2 : 1;
+  e.kind = kind_req ? kind_req : tb_ ? 2 : 1;  // 3: K+1-step sweeps (long-major)
   e.buf = cur();
   e.parity = (int)(issued_ & 1);
   e.sparity = (int)(nsweep_ & 1);
@@ -1894,11 +1894,17 @@ Solver::GraphEntry* Solver::build_graph(int G) {
       ev_wait(kComm, EV_FORK);
       ev_wait(kReduce, EV_FORK);
     }
-    last_kind_ = e.kind;
+    last_kind_ = e.kind == 3 ? 2 : e.kind;
     if (e.kind == 2) {
       for (int i = 0; i < G / K_; ++i) {
         enqueue_multi(cur_);
         issued_ += K_;
+        cur_ = nxt(cur_);
+      }
+    } else if (e.kind == 3) {
+      for (int i = 0; i < G / (K_ + 1); ++i) {
+        enqueue_multi(cur_, K_ + 1);
+        issued_ += K_ + 1;
         cur_ = nxt(cur_);
       }
     } else {
@@ -1952,8 +1958,20 @@ Solver::GraphEntry* Solver::build_graph(int G) {
 
 void Solver::prepare_steps(int64_t n) {
   if (!graphs_allowed()) return;
-  const int G = graph_len_for(n - (int64_t)long_sweeps_for(n) * (K_ + 1));
+  const int nlong = long_sweeps_for(n);
+  const int G = graph_len_for(n - (int64_t)nlong * (K_ + 1));
   if (G > 0 && !find_graph(G)) build_graph(G);
+  // long-major: the first graph of long sweeps (run_chunk issues them after
+  // the K-step part, whose graph ends on the same buffer it started from)
+  const int m = std::min(nlong, long_graph_cap());
+  if (long_major_ && !multi_stream() && m > 0 && G % (2 * K_) == 0 && !find_graph(m * (K_ + 1), 3))
+    build_graph(m * (K_ + 1), 3);
+}
+
+// long-major graphs: at most this many K+1-step sweeps each (the graph chunk)
+int Solver::long_graph_cap() const {
+  const int chunk = cfg_.graph_chunk > 0 ? cfg_.graph_chunk : 32;
+  return std::max(1, chunk / (K_ + 1));
 }
 
 void Solver::run_chunk(int64_t n) {
@@ -2018,7 +2036,32 @@ void Solver::run_chunk(int64_t n) {
     cur_ = nxt(cur_);
     --n;
   }
-  for (int i = 0; i < nlong; ++i) {
+  // long sweeps: long-major runs replay graphs of up to long_graph_cap() of
+  // them (single-stream schedules), else eagerly
+  int left = nlong;
+  while (graphs && long_major_ && !multi_stream() && left > 0) {
+    const int m = std::min(left, long_graph_cap());
+    GraphEntry* g = find_graph(m * (K_ + 1), 3);
+    if (!g) g = build_graph(m * (K_ + 1), 3);
+    if (!g) break;
+    H3D_TRACE("launch_graph long x" << m << " issued=" << issued_);
+    join_pipeline();
+    be_->launch_graph(g->exec);
+    ++graph_launches_;
+    for (int i = 0; i < m; ++i) {
+      record_segment(issued_, K_ + 1, cur());
+      issued_ += K_ + 1;
+      cur_ = nxt(cur_);
+    }
+    left -= m;
+    last_kind_ = 2;
+    last_bnd_ = 0;
+    for (int i = 0; i < EV_COUNT; ++i) ev_valid_[i] = false;
+    ev_record(EV_FORK, kCompute);
+    ev_wait(kComm, EV_FORK);
+    ev_wait(kReduce, EV_FORK);
+  }
+  for (int i = 0; i < left; ++i) {
     record_segment(issued_, K_ + 1, cur());
     enqueue_multi(cur(), K_ + 1);
     issued_ += K_ + 1;
@@ -2064,7 +2107,8 @@ RunResult Solver::run() {
   // joins the streams (the overlapped schedule drains its pipeline there)
   int64_t K = std::max(1, cfg_.check_every);
   if (tb_) {
-    const int64_t cyc = (int64_t)K_ * (nbuf_ == 3 ? 6 : 2);
+    // long-major: chunks of whole K+1-step sweeps too (24 = 6 x 4)
+    const int64_t cyc = (int64_t)K_ * (nbuf_ == 3 ? 6 : 2) * (long_major_ ? K_ + 1 : 1);
     if (graphs_allowed()) K = std::max<int64_t>(K, graph_len_for(INT32_MAX));
     K = std::max(cyc, K - K % cyc);
   }

@@ -323,8 +323,9 @@ class Solver {
     int G = 0, kind = 1, buf = 0, parity = 0, sparity = 0;
     bool first = false;  // captured at iteration 0 (its first sweep computes every residual)
   };
-  GraphEntry* find_graph(int G);
-  GraphEntry* build_graph(int G);
+  GraphEntry* find_graph(int G, int kind = 0);
+  GraphEntry* build_graph(int G, int kind = 0);
+  int long_graph_cap() const;
   void destroy_graphs();
   InitParams init_params(const Local& l) const;
 
