@@ -1052,9 +1052,12 @@ void Solver::calibrate_remainders() {
   const double tk = cost[K_], tl = cost[K_ + 1];
   // long-major: where a K+1 sweep costs less per step than a K one (one
   // subdomain: the last-residual K = 4 sweep at 1022^3, 4.18 against 3.29 ms
-  // for K = 3), step counts run as many long sweeps as they can
+  // for K = 3; not the 8-GPU slab share, whose 122-plane interior packs K + 1
+  // tiles badly), step counts run as many long sweeps as they can
   // (long_sweeps_for)
-  long_major_ = !has_halo_ && local_.size() == 1 && tl < 1e30 && tl / (K_ + 1) < tk / K_;
+  // (with halos the same 15 % margin as the remainder vote below; every rank
+  // must agree: slot 0 of the vote)
+  long_major_ = (!has_halo_ || long_halo_) && tl < 1e30 && tl / (K_ + 1) * (has_halo_ ? 1.15 : 1.0) < tk / K_;
   // votes for the partial sweep, one slot per remainder; the ranks agree on
   // the max: long only where no rank found the partial sweep cheaper (the
   // halo depth of every exchange must match between neighbours)
@@ -1067,6 +1070,7 @@ void Solver::calibrate_remainders() {
   const double margin = has_halo_ ? 1.15 : 1.0;
   std::vector<unsigned long long> partial(K_, 0);
   for (int r = 1; r < K_; ++r) partial[r] = r * (tl - tk) * margin < cost[r] ? 0 : 1;
+  partial[0] = long_major_ ? 0 : 1;
   if (!comm_->all_local() && comm_->size() > 1) {
     void* d = be_->alloc(sizeof(unsigned long long) * K_);
     be_->copy(d, partial.data(), sizeof(unsigned long long) * K_, CopyKind::H2D, kReduce);
@@ -1075,6 +1079,7 @@ void Solver::calibrate_remainders() {
     be_->sync(kReduce);
     be_->release(d);
   }
+  long_major_ = partial[0] == 0;
   long_rem_ = 0;
   for (int r = 1; r < K_; ++r)
     if (!partial[r]) long_rem_ |= 1u << r;

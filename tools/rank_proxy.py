@@ -115,6 +115,7 @@ def main() -> int:
            "mem_used_gb": gb(s.native.mem_free_before - free_after) if free_after is not None else None,
            "phases": phases,
            "long_remainders": list(s.native.long_remainders),
+           "long_major": bool(s.native.long_major),
            "sweep_costs_ms": {k: round(v, 4) for k, v in s.native.sweep_costs.items()},
            "x_schedules": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in t.items()}
                            for t in heat3d_amd.native().tuned_schedules()]}
