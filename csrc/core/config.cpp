@@ -118,7 +118,9 @@ std::string Config::usage() {
      << "  --no-long-sweeps          step-count remainders as partial sweeps, not K+1-step sweeps\n"
      << "  --long-sweeps auto|on|off remainders as K+1-step sweeps: auto = where the start-up timing of\n"
      << "                            the sweeps finds them cheaper than a partial sweep (default auto;\n"
-     << "                            GPU only, measure = on any backend)\n"
+     << "                            GPU only, measure = on any backend; major = step counts as\n"
+     << "                            K+1-step sweeps wherever they fit, as auto does where they are\n"
+     << "                            cheaper per step)\n"
      << "  --autotune auto|on|off    time the sweep schedule candidates (z stride, x segments) at start-up;\n"
      << "                            auto: single-subdomain runs (--no-autotune = off)\n"
      << "  --stream-graphs auto|on|off  the overlapped multi-stream schedule as one linear hipGraph per\n"
@@ -269,7 +271,8 @@ Config Config::parse(int argc, const char* const* argv) {
       else if (v == "on") c.long_sweeps = 1;
       else if (v == "off") c.long_sweeps = 0;
       else if (v == "measure") c.long_sweeps = 2;  // time the sweeps on any backend (tests)
-      else throw UsageError("--long-sweeps takes auto, on, off or measure");
+      else if (v == "major") c.long_sweeps = 3;    // measure, and run long-major whatever the timing
+      else throw UsageError("--long-sweeps takes auto, on, off, measure or major");
     }
     else if (key == "--no-autotune") c.autotune = 0;
     else if (key == "--autotune") {

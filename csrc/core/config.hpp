@@ -81,7 +81,8 @@ struct Config {
   bool block_overlap = true;      // block decompositions: interior || halo (false: exchange first)
   // K+1-step sweeps absorb step counts that are not multiples of K: -1 auto
   // (GPU: where timed at start-up cheaper than the partial sweep), 1 always, 0
-  // never, 2 timed on any backend (tests of the rank vote on the CPU)
+  // never, 2 timed on any backend (tests of the rank vote on the CPU), 3 as 2
+  // and long-major (Solver::long_sweeps_for) whatever the timing
   int long_sweeps = -1;
   // time the interior sweeps' schedule candidates at initialisation: -1 auto
   // (single-subdomain runs, whose sweeps run alone as they are timed), 0 off, 1 on

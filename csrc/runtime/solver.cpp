@@ -1057,7 +1057,8 @@ void Solver::calibrate_remainders() {
   // (long_sweeps_for)
   // (with halos the same 15 % margin as the remainder vote below; every rank
   // must agree: slot 0 of the vote)
-  long_major_ = (!has_halo_ || long_halo_) && tl < 1e30 && tl / (K_ + 1) * (has_halo_ ? 1.15 : 1.0) < tk / K_;
+  long_major_ = (!has_halo_ || long_halo_) && tl < 1e30 &&
+                (cfg_.long_sweeps == 3 || tl / (K_ + 1) * (has_halo_ ? 1.15 : 1.0) < tk / K_);
   // votes for the partial sweep, one slot per remainder; the ranks agree on
   // the max: long only where no rank found the partial sweep cheaper (the
   // halo depth of every exchange must match between neighbours)

@@ -158,7 +158,7 @@ def native_rccl_gpu_worker(rank, world, port, outdir, n, eps, decomp, dtype, ext
     dist.destroy_process_group()
 
 
-def native_socket_policy_worker(rank, world, port, outdir, n, eps, decomp):
+def native_socket_policy_worker(rank, world, port, outdir, n, eps, decomp, mode="measure"):
     """Remainder policy across real processes: every rank times its sweeps
     (--long-sweeps measure), the ranks vote over the socket transport, and
     run() (with a --time-limit iteration cap agreed by one more all-reduce)
@@ -169,12 +169,12 @@ def native_socket_policy_worker(rank, world, port, outdir, n, eps, decomp):
     import heat3d_amd
 
     s = heat3d_amd.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu", decomp=decomp, threads=1,
-                              extra_args=["--temporal", "3", "--long-sweeps", "measure", "--time-limit", "60",
+                              extra_args=["--temporal", "3", "--long-sweeps", mode, "--time-limit", "60",
                                           "--check-every", "6"])
     s.initialize()
     with open(os.path.join(outdir, f"policy{rank}.json"), "w") as f:
         json.dump({"long": list(s.native.long_remainders), "costs": dict(s.native.sweep_costs),
-                   "long_halo": s.native.long_halo_sweeps}, f)
+                   "long_halo": s.native.long_halo_sweeps, "long_major": s.native.long_major}, f)
     # a step count with remainder 2 (long or partial per the vote), then run on
     s.step(20)
     r = s.run()

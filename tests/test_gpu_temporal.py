@@ -539,6 +539,35 @@ def test_long_sweeps_across_halos_gpu(h3d, gpu, vr, dims, dtype):
     assert a.native.verify_halos() == 0
 
 
+@pytest.mark.parametrize("vr,dims", [(1, (1, 1, 1)), (3, (3, 1, 1)), (8, (2, 2, 2)), (4, (1, 2, 2))])
+def test_long_major_gpu(h3d, gpu, vr, dims):
+    """--long-sweeps major: step counts run as many K+1-step (last-residual)
+    sweeps as fit, across halos too; bitwise equal to single steps, and run()
+    converges at the single steps' iteration (the replay of a long sweep)."""
+    n = (82, 70, 150)
+    kw = dict(virtual_ranks=vr, decomp=dims) if vr > 1 else {}
+    a = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="hip", extra_args=["--long-sweeps", "major"], **kw)
+    b = h3d.HeatSolver(n, 10 ** 6, 0.0, backend="hip", extra_args=["--temporal", "1"])
+    a.initialize(), b.initialize()
+    assert a.native.long_major
+    for k in (5, 20, 11, 24):
+        a.step(k)
+        b.step(k)
+        a.synchronize(), b.synchronize()
+        sa, sb = a.native.state(), b.native.state()
+        assert sa["iter"] == sb["iter"] and sa["last_residual"] == sb["last_residual"]
+        assert np.array_equal(a.gather(), b.gather()), (vr, dims, k)
+    if vr > 1:
+        assert a.native.verify_halos() == 0
+    for eps in (3e-4, 2.9e-4):
+        c = h3d.HeatSolver(n, 10 ** 6, eps, backend="hip", extra_args=["--long-sweeps", "major"], **kw)
+        d = h3d.HeatSolver(n, 10 ** 6, eps, backend="hip", extra_args=["--temporal", "1"])
+        rc, rd = c.run(), d.run()
+        assert rc["converged"] and rc["conv_iter"] == rd["conv_iter"], (eps, rc, rd)
+        assert rc["last_residual"] == rd["last_residual"]
+        assert np.array_equal(c.gather(), d.gather())
+
+
 @pytest.mark.parametrize("vr,dims,n", [(8, (2, 2, 2), (82, 180, 260)), (4, (1, 2, 2), (40, 180, 380)),
                                         (4, (2, 2, 1), (90, 180, 100))])
 @pytest.mark.parametrize("dtype,thin", [("fp64", False), ("fp32", False), ("fp64", True)])

@@ -110,8 +110,9 @@ def test_staged_comm_cpu(h3d, tmp_path, world, decomp, temporal):
     assert np.array_equal(np.load(tmp_path / "field.npy"), single.gather())
 
 
-@pytest.mark.parametrize("world,decomp", [(2, (2, 1, 1)), (3, (3, 1, 1))])
-def test_remainder_policy_vote_across_processes(h3d, tmp_path, world, decomp):
+@pytest.mark.parametrize("world,decomp,mode", [(2, (2, 1, 1), "measure"), (3, (3, 1, 1), "measure"),
+                                               (2, (2, 1, 1), "major"), (3, (1, 3, 1), "major")])
+def test_remainder_policy_vote_across_processes(h3d, tmp_path, world, decomp, mode):
     """Solver::calibrate_remainders across real processes: each rank times
     its sweeps, the ranks agree by an all-reduce (their halo exchanges must
     pair up: a long sweep exchanges K+1 planes), and the solve stays bitwise
@@ -121,9 +122,11 @@ def test_remainder_policy_vote_across_processes(h3d, tmp_path, world, decomp):
     from _mp_workers import native_socket_policy_worker
 
     n, eps = 31, 1e-4
-    _spawn(native_socket_policy_worker, world, str(tmp_path), n, eps, decomp)
+    _spawn(native_socket_policy_worker, world, str(tmp_path), n, eps, decomp, mode)
     pol = [json.loads((tmp_path / f"policy{r}.json").read_text()) for r in range(world)]
     assert all(p["long_halo"] for p in pol)
+    # major: long-major sweeps (every step count as many K+1-step sweeps as fit)
+    assert all(p["long_major"] == (mode == "major") for p in pol), pol
     assert all(set(p["costs"]) == {"sweep3", "sweep4", "step", "sweep2"} for p in pol), pol
     assert all(p["long"] == pol[0]["long"] for p in pol), pol  # one decision for the job
     single = h3d.HeatSolver((n, n, n), 10 ** 6, eps, backend="cpu")
