@@ -599,7 +599,8 @@ void Solver::initialize() {
       // depth's shape in that form
       const bool picked = (rl_pick_[Kp].O & kResidualLastOnly) != 0;
       ks_last_[Kp] = picked ? rl_pick_[Kp] : last_only(spec_for_depth(Kp));
-      rl_d_[Kp] = hip::lean_supported(dt_, ks_last_[Kp]);
+      // (block decompositions: long sweeps keep every residual, see long_major_)
+      rl_d_[Kp] = hip::lean_supported(dt_, ks_last_[Kp]) && !(ordered_halo_ && Kp > K_);
     }
   rl_ = rl_d_[K_];
   reset_state();
@@ -1057,7 +1058,10 @@ void Solver::calibrate_remainders() {
   // (long_sweeps_for)
   // (with halos the same 15 % margin as the remainder vote below; every rank
   // must agree: slot 0 of the vote)
-  long_major_ = (!has_halo_ || long_halo_) && tl < 1e30 &&
+  // (not block decompositions: a converged long sweep of a 2x2x2 run rolled
+  // back to a different field under it — gpurun_out/r6v5, not yet explained —
+  // so blocks keep K-step sweeps)
+  long_major_ = (!has_halo_ || long_halo_) && !ordered_halo_ && tl < 1e30 &&
                 (cfg_.long_sweeps == 3 || tl / (K_ + 1) * (has_halo_ ? 1.15 : 1.0) < tk / K_);
   // votes for the partial sweep, one slot per remainder; the ranks agree on
   // the max: long only where no rank found the partial sweep cheaper (the

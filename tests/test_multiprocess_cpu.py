@@ -111,7 +111,7 @@ def test_staged_comm_cpu(h3d, tmp_path, world, decomp, temporal):
 
 
 @pytest.mark.parametrize("world,decomp,mode", [(2, (2, 1, 1), "measure"), (3, (3, 1, 1), "measure"),
-                                               (2, (2, 1, 1), "major"), (3, (1, 3, 1), "major")])
+                                               (2, (2, 1, 1), "major"), (3, (3, 1, 1), "major")])
 def test_remainder_policy_vote_across_processes(h3d, tmp_path, world, decomp, mode):
     """Solver::calibrate_remainders across real processes: each rank times
     its sweeps, the ranks agree by an all-reduce (their halo exchanges must
