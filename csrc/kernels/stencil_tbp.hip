@@ -539,6 +539,8 @@ static bool run_tbp(const StencilParams* p, const KernelSpec& k, hipStream_t s) 
     // output-store cache policy (spec field 7), default shape only
     H3D_TBP(3, 16, 3, 3, 2) H3D_TBP(3, 16, 3, 3, 3) H3D_TBP(3, 16, 3, 3, 17) H3D_TBP(3, 16, 3, 3, 19)
     H3D_TBP(3, 16, 3, 3, 2 | kResidualLastOnly)
+    // the long (K = 4) and partial (K = 2) sweeps' default shapes, last residual only
+    H3D_TBP(2, 16, 4, 3, kResidualLastOnly) H3D_TBP(2, 16, 2, 3, kResidualLastOnly)
     H3D_TBP(3, 16, 3, 3, 0) H3D_TBP(3, 16, 3, 4, 0) H3D_TBP(2, 16, 3, 3, 0) H3D_TBP(2, 16, 4, 3, 0)
     H3D_TBP(2, 16, 4, 4, 0) H3D_TBP(3, 16, 4, 3, 0) H3D_TBP(2, 16, 2, 3, 0) H3D_TBP(3, 16, 2, 3, 0)
   } else {

@@ -113,8 +113,8 @@ VARIANTS_K = {3: ["tl3", "tl3:1:3:1:16:0:4", "tl3:1:2:1:16:0:3", "tl3:1:3:1:16:5
               2: ["tl2", "tl2:1:2:1:16:0:3", "tl2:1:5:1:16:0:3:2", "tl2:1:5:1:16:0:3:66", "tl2:1:3:1:16:0:3:66"]}
 # fp32: tlK:2:… is the packed-pair lean kernel (stencil_tbp.hip)
 PAIR = {3: ["tl3:2:3:1:16:0:3", "tl3:2:3:1:16:0:3:2", "tl3:2:3:1:16:0:3:66", "tl3:2:3:1:16:0:4", "tl3:2:2:1:16:0:3", "tl3:2:3:1:16:5:3"],
-        4: ["tl4:2:2:1:16:0:3", "tl4:2:2:1:16:0:4", "tl4:2:2:1:16:7:3"],
-        2: ["tl2:2:2:1:16:0:3", "tl2:2:3:1:16:0:3"]}
+        4: ["tl4:2:2:1:16:0:3", "tl4:2:2:1:16:0:4", "tl4:2:2:1:16:7:3", "tl4:2:2:1:16:0:3:64"],
+        2: ["tl2:2:2:1:16:0:3", "tl2:2:3:1:16:0:3", "tl2:2:2:1:16:0:3:64"]}
 VARIANTS_K_F32 = PAIR
 
 
