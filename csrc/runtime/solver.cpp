@@ -1059,8 +1059,10 @@ void Solver::calibrate_remainders() {
   // (with halos the same 15 % margin as the remainder vote below; every rank
   // must agree: slot 0 of the vote)
   // (not block decompositions: a converged long sweep of a 2x2x2 run rolled
-  // back to a different field under it — gpurun_out/r6v5, not yet explained —
-  // so blocks keep K-step sweeps)
+  // back to a different field under it on the GPU — gpurun_out/r6v5, and with
+  // every residual in the long sweeps too, r6lb — while the CPU backend's
+  // 2x2x2 / 1x2x2 long-major runs were bitwise; not yet explained, so blocks
+  // keep K-step sweeps)
   long_major_ = (!has_halo_ || long_halo_) && !ordered_halo_ && tl < 1e30 &&
                 (cfg_.long_sweeps == 3 || tl / (K_ + 1) * (has_halo_ ? 1.15 : 1.0) < tk / K_);
   // votes for the partial sweep, one slot per remainder; the ranks agree on
